@@ -1,0 +1,144 @@
+/*
+ * pbgpu.h — C ABI of the MI355X packet-build library (libpbgpu.so).
+ *
+ * Drop-in seam: the reference builds one frame per loop iteration inside
+ * thread_hdl() (src/sequence.c:433-602) and hands each one to
+ * send_packet(xsk, thread_id, buffer, len, verbose) (src/af_xdp.h:59,
+ * src/sequence.c:607).  This library replaces the build side of that seam:
+ * a batch of iterations is built on the GPU into device-resident frames, then
+ * landed in the (pinned) AF_XDP UMEM, after which the host fills TX
+ * descriptors exactly as af_xdp.c:217-227 does.
+ *
+ * Conventions follow the reference's C code: plain C, int
+ * returns (0 = ok, negative errno-style codes), pointer out-params for setup,
+ * no exit(), diagnostics on stderr only when PBGPU_VERBOSE is set.
+ *
+ *   reference interface                         replaced / mirrored by
+ *   ------------------------------------------  ----------------------------
+ *   thread_hdl() prologue: MAC/proto parse,     pbgpu_load_sequence()
+ *     template + payload prep (sequence.c:66-374)
+ *   thread_hdl() hot loop body                  pbgpu_build()
+ *     (sequence.c:433-602), one call per batch
+ *   send_packet() memcpy into UMEM slot          pbgpu_copy_to_umem()
+ *     (af_xdp.c:200-214)
+ *   total_pckts/total_bytes __sync counters     pbgpu_counters()
+ *     (sequence.c:12-14, 633-642)
+ *   pthread fan-out, one socket per thread      one pbgpu_ctx per GPU
+ *     (sequence.c:741-762)                        (packets sharded by index)
+ */
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "pb_config.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes (negative errno values, as the reference reports errno) */
+#define PBGPU_OK 0
+#define PBGPU_ENOENT (-2)     /* sequence slot not loaded */
+#define PBGPU_EIO (-5)        /* HIP runtime error */
+#define PBGPU_ENOMEM (-12)
+#define PBGPU_EINVAL (-22)    /* bad config (e.g. min > max, no dst_ip) */
+#define PBGPU_ENOSPC (-28)    /* frames buffer too small */
+#define PBGPU_ENODEV (-19)    /* no such GPU */
+#define PBGPU_ENOTSUP (-95)   /* valid config this build does not run on the GPU */
+
+typedef struct pbgpu_ctx pbgpu_ctx;
+
+/* Device-resident output of one pbgpu_build() call.
+ * Frame f (0 <= f < n_frames) occupies bytes
+ *   [offset(f), offset(f) + len(f)) of `data`, packed back to back, where
+ *   fixed_len > 0 : offset(f) = f * fixed_len, len(f) = fixed_len
+ *   fixed_len == 0: offset(f) = offsets[f], len(f) = offsets[f+1] - offsets[f]
+ * Frames are numbered iteration-major: f = (k - first_iter) * pl_cnt + i for
+ * payload i of iteration k (the reference's inner loop, sequence.c:530). */
+typedef struct pbgpu_frames
+{
+    uint8_t *data;          /* device pointer, capacity_bytes (16-B padded) */
+    uint64_t *offsets;      /* device pointer, capacity_frames + 1 entries */
+    uint32_t *tile_first;   /* device scratch (variable-length tiling) */
+    uint64_t *scan_tmp;     /* device scratch (length scan) */
+    uint64_t capacity_frames;
+    uint64_t capacity_bytes;
+
+    /* filled by pbgpu_build() */
+    uint16_t seq_idx;
+    uint64_t first_iter;
+    uint64_t n_frames;
+    uint32_t fixed_len;     /* 0 -> variable length, see offsets */
+    uint64_t total_bytes;   /* exact for fixed length; UINT64_MAX until
+                               pbgpu_frames_total() for variable length */
+} pbgpu_frames;
+
+/* ---- context (one per GPU; not thread-safe within one ctx) ---- */
+int pbgpu_open(int device, pbgpu_ctx **out);
+void pbgpu_close(pbgpu_ctx *ctx);
+const char *pbgpu_strerror(int err);
+int pbgpu_device_count(int *n);
+
+/* ---- setup: compile one sequence into its GPU template ----
+ * src_mac / dst_mac: resolved MACs (the reference resolves missing ones with
+ * get_src_mac_address / get_gw_mac, sequence.c:111-130); NULL -> parse
+ * seq->eth strings, unset -> 00:00:00:00:00:00.
+ * rules: NULL -> { PB_PAYLOAD_STREAM, PB_FOLD_FULL }. */
+int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *seq,
+                        const uint8_t *src_mac, const uint8_t *dst_mac, const pb_rules_t *rules,
+                        uint64_t seed_base);
+
+/* Upper bounds of frames / bytes produced by n_iter iterations. */
+int pbgpu_build_size(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t n_iter,
+                     uint64_t *max_frames, uint64_t *max_bytes);
+
+int pbgpu_frames_alloc(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capacity_bytes,
+                       pbgpu_frames **out);
+void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *frames);
+
+/* ---- hot path: build iterations [first_iter, first_iter + n_iter) ----
+ * Asynchronous on the context's stream.  Seeds: pb_config.h seed stream with
+ * the seed_base given to pbgpu_load_sequence(). */
+int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter,
+                pbgpu_frames *out);
+
+int pbgpu_sync(pbgpu_ctx *ctx);
+int pbgpu_frames_total(pbgpu_ctx *ctx, pbgpu_frames *frames, uint64_t *total_bytes);
+
+/* ---- landing: device -> host ---- */
+int pbgpu_copy_packed(pbgpu_ctx *ctx, const pbgpu_frames *frames, void *host_dst,
+                      uint64_t byte_offset, uint64_t nbytes);
+int pbgpu_copy_offsets(pbgpu_ctx *ctx, const pbgpu_frames *frames, uint64_t *host_dst);
+/* UMEM landing (af_xdp.c:200-214 geometry): frame first_frame + j lands at
+ * umem + (first_slot + j) * slot_stride; lens_out[j] = its length.  `umem`
+ * may be any host pointer; pbgpu_host_register() it first for full speed. */
+int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *frames, void *umem, uint32_t slot_stride,
+                       uint32_t first_slot, uint64_t first_frame, uint32_t n, uint16_t *lens_out);
+int pbgpu_host_register(pbgpu_ctx *ctx, void *ptr, size_t bytes);
+int pbgpu_host_unregister(pbgpu_ctx *ctx, void *ptr);
+
+/* ---- counters (sequence.c:12-14, 633-642): frames / bytes built per
+ * sequence since open; multi-GPU callers all-reduce these over RCCL. ---- */
+int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq);
+
+/* ---- measurement ---- */
+/* Device time of the frame-build kernels launched since the last call:
+ * sum over launches (ms) and launch count (HIP events on the ctx stream). */
+int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches);
+/* Write-only roofline probe: `reps` launches of a non-temporal 16-B/lane
+ * fill over `bytes`; returns the mean device time per launch. */
+int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_launch);
+/* Build-kernel tile size chosen for a sequence (bytes per workgroup). */
+int pbgpu_tile_bytes(pbgpu_ctx *ctx, uint16_t seq_idx, uint32_t *tile_bytes);
+
+/* ABI self-description for FFI bindings: sizes / offsets of the structs above.
+ * which: 0 sizeof(pb_sequence_t), 1 sizeof(pb_payload_opt_t), 2 sizeof(pbgpu_frames),
+ *        3 offsetof(pb_sequence_t, ip.ranges), 4 offsetof(pb_sequence_t, pls),
+ *        5 offsetof(pb_sequence_t, pl_cnt), 6 offsetof(pbgpu_frames, total_bytes);
+ * returns 0 for an unknown index. */
+size_t pbgpu_abi_size(int which);
+
+#ifdef __cplusplus
+}
+#endif

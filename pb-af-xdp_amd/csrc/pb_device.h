@@ -1,0 +1,138 @@
+// pb_device.h — device-side data layout and arithmetic shared by the frame-
+// build kernels (pbgpu_kernels.hip).  CDNA4 / gfx950 only.
+//
+// Reference arithmetic restated:
+//   rand_r        glibc, 3 LCG steps          (call sites sequence.c:345-554)
+//   rand_num      min + rand_r(copy) % (max-min+1)   (PB-Common, un-vendored)
+//   rand_ip       (net & ~hm) | (r0 & hm)             (PB-Common, un-vendored)
+//   checksums     RFC 1071 in the little-endian word domain, as csum.h does
+//                 on x86 (sequence.c:569-602)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PB_WG 256                          // threads per workgroup (4 waves)
+#define PB_CPL 4                           // 16-B chunks per lane per tile
+#define PB_TILE_MAX (PB_WG * PB_CPL * 16)  // 16 KiB of output per workgroup
+#define PB_NF_MAX 260                      // frames touching one tile, max
+#define PB_IMG_DW 16                       // header image: 64 B per frame
+#define PB_JNEG 16                         // jump table starts at j = -16
+
+// glibc LCG
+#define PB_LCG_A 1103515245u
+#define PB_LCG_C 12345u
+
+enum pb_kflags : uint32_t
+{
+    PBK_RND_TTL = 1u << 0,
+    PBK_RND_ID = 1u << 1,
+    PBK_RND_SADDR = 1u << 2,
+    PBK_RND_SPORT = 1u << 3,
+    PBK_RND_DPORT = 1u << 4,
+    PBK_IP_CSUM = 1u << 5,
+    PBK_L4_CSUM = 1u << 6,
+    PBK_IPH_SINGLE = 1u << 7,
+    PBK_LITERAL = 1u << 8,
+    PBK_SUM_IN_A = 1u << 9,   // payload sums computed per frame in phase A
+    PBK_PSEUDO = 1u << 10,    // UDP/TCP pseudo header (not ICMP)
+};
+
+// n % d for n < 2^31 by multiply-shift (Granlund-Montgomery, N = 31):
+// m = ceil(2^(31+l) / d), l = ceil(log2 d), sh = 31 + l.
+struct pb_div
+{
+    uint32_t d, m, sh;
+};
+
+// one payload of the sequence (sequence_t.pls[i] after setup)
+struct pb_pl
+{
+    uint32_t random;   // 1: length + bytes drawn per iteration
+    uint32_t min_len;
+    pb_div len;        // divisor max_len - min_len + 1
+    uint32_t blob_off; // static bytes at blob + blob_off (16-B zero pad around)
+    uint32_t slen;     // static length
+    uint32_t ssum;     // static bytes' little-endian 16-bit word sum (unfolded)
+};
+
+struct pb_kargs
+{
+    uint32_t tmpl[16];  // header template bytes 0..63 as LE dwords, random fields 0
+    uint32_t flags;
+    uint32_t hl;        // 42 (UDP, ICMP) or 54 (TCP)
+    uint32_t l4len;     // 8 or 20
+    uint32_t proto;
+    uint32_t csum_dw;   // image dword holding the L4 checksum
+    uint32_t csum_hi;   // 1: checksum in the high half of that dword
+    uint32_t ttl_min;
+    pb_div ttl;
+    uint32_t id_min;
+    pb_div id;
+    pb_div rng;
+    pb_div port;        // 65535
+    const uint2 *ranges; // {net & ~hm, hm} host order
+    uint32_t pl_cnt;
+    pb_pl pl0;
+    const pb_pl *pls;
+    const uint8_t *blob;
+    const uint2 *jump;  // jump[j + PB_JNEG] = (A, C): state_j = A * st0 + C = L^(3(j+1))(st0)
+    uint64_t seed_base;
+    uint32_t seq;
+    uint64_t first_iter;
+    uint64_t n_frames;
+    uint64_t total_bytes;   // fixed length only
+    uint32_t fixed_len;     // 0 -> variable
+    pb_div flen;            // division by fixed_len
+    const uint64_t *offsets;
+    const uint32_t *tile_first;
+    uint32_t tile_bytes;
+    uint32_t n_tiles;
+    uint8_t *out;
+    unsigned long long *counters; // [2] pckts, bytes of this sequence
+};
+
+__device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)
+{
+    uint32_t q = (uint32_t)(((uint64_t)n * v.m) >> v.sh);
+    return n - q * v.d;
+}
+
+__device__ __forceinline__ uint32_t pb_divq(uint32_t n, const pb_div &v)
+{
+    return (uint32_t)(((uint64_t)n * v.m) >> v.sh);
+}
+
+// glibc rand_r on a copy of the seed (PB-Common rand_num takes it by value).
+__device__ __forceinline__ uint32_t pb_rand_r(uint32_t s)
+{
+    uint32_t n1 = s * PB_LCG_A + PB_LCG_C;
+    uint32_t n2 = n1 * PB_LCG_A + PB_LCG_C;
+    uint32_t n3 = n2 * PB_LCG_A + PB_LCG_C;
+    return (((n1 >> 16) & 0x7FFu) << 20) ^ (((n2 >> 16) & 0x3FFu) << 10) ^ ((n3 >> 16) & 0x3FFu);
+}
+
+__device__ __forceinline__ uint32_t pb_seed(uint64_t seed_base, uint32_t seq, uint64_t k)
+{
+    uint64_t z = (seed_base ^ (((uint64_t)seq << 48) + k)) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (uint32_t)(z ^ (z >> 31));
+}
+
+__device__ __forceinline__ uint32_t pb_bswap16(uint32_t v)
+{
+    return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu);
+}
+
+__device__ __forceinline__ uint32_t pb_fold(uint32_t s)
+{
+    s = (s & 0xFFFFu) + (s >> 16);
+    s = (s & 0xFFFFu) + (s >> 16);
+    return s;
+}
+
+__device__ __forceinline__ uint32_t pb_halves(uint32_t d)
+{
+    return (d & 0xFFFFu) + (d >> 16);
+}

@@ -1,0 +1,1013 @@
+// pbgpu.cpp — C-ABI shim of libpbgpu.so (include/pbgpu.h).
+//
+// Host side of the drop-in seam: compiles a sequence (PB-Common sequence_t
+// mirror, include/pb_config.h) into the GPU template once — the work the
+// reference does in thread_hdl()'s prologue, src/sequence.c:66-374 — then
+// launches the frame-build kernels per batch (the loop body,
+// sequence.c:433-602) and lands frames in host memory for the AF_XDP TX path
+// (af_xdp.c:200-227).  The product path has no CPU frame builder: if the HIP
+// runtime or the device is missing every entry point fails with an error.
+#include <arpa/inet.h>
+#include <ctype.h>
+#include <stddef.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/pbgpu.h"
+#include "pb_device.h"
+
+extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid, hipStream_t st);
+extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
+                                         uint64_t *offsets, uint32_t *tile_first, uint32_t tile_shift,
+                                         hipStream_t st);
+extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *offsets, uint64_t first, uint32_t n,
+                                         uint8_t *dst, uint32_t stride, uint16_t *lens, hipStream_t st);
+extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, hipStream_t st);
+
+#define PB_JUMP_N (65536 + 64) // entries j = -16 .. 65583
+#define PB_SCAN_FRAMES_PER_BLOCK (256 * 8)
+
+namespace
+{
+
+int verbose()
+{
+    static int v = -1;
+    if (v < 0)
+        v = getenv("PBGPU_VERBOSE") != NULL;
+    return v;
+}
+
+#define HIPCHK(call)                                                                         \
+    do                                                                                       \
+    {                                                                                        \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess)                                                                \
+        {                                                                                    \
+            if (verbose())                                                                   \
+                fprintf(stderr, "[pbgpu] %s:%d %s -> %s\n", __FILE__, __LINE__, #call,       \
+                        hipGetErrorString(e_));                                              \
+            return PBGPU_EIO;                                                                \
+        }                                                                                    \
+    } while (0)
+
+struct seq_slot
+{
+    bool loaded = false;
+    pb_kargs K;              // template part; per-launch fields patched in pbgpu_build
+    uint32_t fpi = 1;        // frames per iteration
+    uint32_t min_flen = 0, max_flen = 0;
+    uint32_t tile_shift = 14;
+    uint2 *d_ranges = nullptr;
+    pb_pl *d_pls = nullptr;
+    uint8_t *d_blob = nullptr;
+};
+
+struct timing_pair
+{
+    hipEvent_t a, b;
+};
+
+} // namespace
+
+struct pbgpu_ctx
+{
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint2 *d_jump = nullptr;
+    unsigned long long *d_counters = nullptr; // [PB_MAX_SEQUENCES][4]
+    seq_slot seqs[PB_MAX_SEQUENCES];
+    std::vector<timing_pair> pending;
+    std::vector<timing_pair> pool;
+    uint8_t *h_stage = nullptr;
+    size_t h_stage_bytes = 0;
+};
+
+namespace
+{
+
+uint32_t host_rand_r(uint32_t *seed)
+{
+    uint32_t x = *seed, r;
+    x = x * PB_LCG_A + PB_LCG_C;
+    r = (x >> 16) & 0x7FFu;
+    x = x * PB_LCG_A + PB_LCG_C;
+    r = (r << 10) ^ ((x >> 16) & 0x3FFu);
+    x = x * PB_LCG_A + PB_LCG_C;
+    r = (r << 10) ^ ((x >> 16) & 0x3FFu);
+    *seed = x;
+    return r;
+}
+
+uint32_t host_seed(uint64_t seed_base, uint32_t seq, uint64_t k)
+{
+    uint64_t z = (seed_base ^ (((uint64_t)seq << 48) + k)) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (uint32_t)(z ^ (z >> 31));
+}
+
+pb_div make_div(uint32_t d)
+{
+    pb_div v;
+    v.d = d;
+    uint32_t l = 0;
+    while ((1ull << l) < d)
+        ++l;
+    v.sh = 31 + l;
+    v.m = (uint32_t)(((1ull << v.sh) + d - 1) / d);
+    return v;
+}
+
+// jump[j + PB_JNEG] = L^(3(j+1)) as (A, C), j = -PB_JNEG ..
+std::vector<uint2> make_jump_table()
+{
+    const uint32_t a = PB_LCG_A, c = PB_LCG_C;
+    uint32_t ainv = a; // Newton: a * ainv == 1 mod 2^32
+    for (int i = 0; i < 5; ++i)
+        ainv *= 2u - a * ainv;
+    // inverse step y -> ainv * (y - c)
+    const uint32_t ia = ainv, ic = (uint32_t)(0u - ainv * c);
+    // E(-16) = L^(-45)
+    uint32_t A = 1, C = 0;
+    for (int i = 0; i < 3 * (PB_JNEG - 1); ++i)
+    {
+        A = ia * A;
+        C = ia * C + ic;
+    }
+    const uint32_t a3 = a * a * a, c3 = c * (a * a + a + 1u);
+    std::vector<uint2> t(PB_JUMP_N);
+    for (int j = 0; j < PB_JUMP_N; ++j)
+    {
+        t[j] = make_uint2(A, C);
+        A = a3 * A;
+        C = a3 * C + c3;
+    }
+    return t;
+}
+
+int str_ieq(const char *a, const char *b)
+{
+    for (; *a && *b; a++, b++)
+        if (tolower((unsigned char)*a) != tolower((unsigned char)*b))
+            return 0;
+    return *a == *b;
+}
+
+void parse_mac(const char *s, uint8_t mac[6])
+{
+    memset(mac, 0, 6);
+    if (s)
+        sscanf(s, "%hhx:%hhx:%hhx:%hhx:%hhx:%hhx", &mac[0], &mac[1], &mac[2], &mac[3], &mac[4], &mac[5]);
+}
+
+// "<ip>/<cidr>" (strtok semantics, as PB-Common rand_ip splits it); invalid
+// ranges take the reference's fail path, 127.0.0.1 (sequence.c:473-482).
+uint2 compile_range(const char *r)
+{
+    uint2 out = make_uint2(0x7F000001u, 0u);
+    if (r == NULL)
+        return out;
+    char *cpy = strdup(r);
+    if (cpy == NULL)
+        return out;
+    char *save = NULL;
+    char *ip = strtok_r(cpy, "/", &save);
+    char *cs = strtok_r(NULL, "/", &save);
+    struct in_addr a;
+    if (ip && cs && inet_aton(ip, &a))
+    {
+        int cidr = atoi(cs);
+        if (cidr >= 0 && cidr <= 32)
+        {
+            uint32_t hm = cidr == 0 ? 0xFFFFFFFFu : (cidr == 32 ? 0u : ((1u << (32 - cidr)) - 1u));
+            out = make_uint2(ntohl(a.s_addr) & ~hm, hm);
+        }
+    }
+    free(cpy);
+    return out;
+}
+
+// exact payload text -> bytes (sequence.c:269-337)
+int compile_exact(const pb_payload_opt_t *po, std::vector<uint8_t> &bytes)
+{
+    std::vector<char> text;
+    if (po->is_file)
+    {
+        FILE *fp = fopen(po->exact, "rb");
+        if (fp)
+        {
+            fseek(fp, 0, SEEK_END);
+            long n = ftell(fp);
+            fseek(fp, 0, SEEK_SET);
+            text.assign(n > 0 ? (size_t)n + 1 : 1, 0);
+            if (n > 0 && fread(text.data(), 1, (size_t)n, fp) != (size_t)n)
+                text.assign(1, 0);
+            fclose(fp);
+        }
+        else
+        {
+            text.assign(1, 0);
+        }
+    }
+    else
+    {
+        size_t n = strlen(po->exact);
+        text.assign(po->exact, po->exact + n + 1);
+    }
+    bytes.clear();
+    if (po->is_string)
+    {
+        size_t n = strlen(text.data());
+        bytes.assign(text.data(), text.data() + n);
+    }
+    else
+    {
+        char *rest = text.data(), *tok;
+        while ((tok = strtok_r(rest, " ", &rest)) != NULL)
+        {
+            unsigned char b = 0;
+            sscanf(tok, "%2hhx", &b);
+            bytes.push_back(b);
+        }
+    }
+    return bytes.size() > PB_MAX_PCKT_LEN ? PBGPU_EINVAL : PBGPU_OK;
+}
+
+uint32_t le_word_sum(const uint8_t *p, size_t n)
+{
+    uint64_t s = 0;
+    for (size_t j = 0; j < n; ++j)
+        s += (uint64_t)p[j] << ((j & 1) * 8);
+    while (s >> 16)
+        s = (s & 0xFFFF) + (s >> 16);
+    return (uint32_t)s;
+}
+
+template <typename T>
+int upload(T **dptr, const T *src, size_t n)
+{
+    if (*dptr)
+        (void)hipFree(*dptr);
+    *dptr = nullptr;
+    if (n == 0)
+        return PBGPU_OK;
+    HIPCHK(hipMalloc((void **)dptr, n * sizeof(T)));
+    HIPCHK(hipMemcpy(*dptr, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return PBGPU_OK;
+}
+
+void slot_free(seq_slot &s)
+{
+    if (s.d_ranges)
+        (void)hipFree(s.d_ranges);
+    if (s.d_pls)
+        (void)hipFree(s.d_pls);
+    if (s.d_blob)
+        (void)hipFree(s.d_blob);
+    s = seq_slot();
+}
+
+} // namespace
+
+extern "C" {
+
+const char *pbgpu_strerror(int err)
+{
+    switch (err)
+    {
+    case PBGPU_OK: return "ok";
+    case PBGPU_ENOENT: return "sequence not loaded";
+    case PBGPU_EIO: return "HIP runtime error";
+    case PBGPU_ENOMEM: return "out of memory";
+    case PBGPU_EINVAL: return "invalid argument or sequence";
+    case PBGPU_ENOSPC: return "frames buffer too small";
+    case PBGPU_ENODEV: return "no such GPU";
+    case PBGPU_ENOTSUP: return "sequence not supported on the GPU path";
+    default: return "unknown error";
+    }
+}
+
+int pbgpu_device_count(int *n)
+{
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess)
+        c = 0;
+    *n = c;
+    return PBGPU_OK;
+}
+
+int pbgpu_open(int device, pbgpu_ctx **out)
+{
+    if (out == NULL)
+        return PBGPU_EINVAL;
+    *out = NULL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return PBGPU_ENODEV;
+    HIPCHK(hipSetDevice(device));
+    pbgpu_ctx *ctx = new pbgpu_ctx();
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+    {
+        delete ctx;
+        return PBGPU_EIO;
+    }
+    std::vector<uint2> jt = make_jump_table();
+    if (upload(&ctx->d_jump, jt.data(), jt.size()) != PBGPU_OK ||
+        hipMalloc((void **)&ctx->d_counters, sizeof(unsigned long long) * 4 * PB_MAX_SEQUENCES) != hipSuccess ||
+        hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * 4 * PB_MAX_SEQUENCES) != hipSuccess)
+    {
+        pbgpu_close(ctx);
+        return PBGPU_EIO;
+    }
+    *out = ctx;
+    return PBGPU_OK;
+}
+
+void pbgpu_close(pbgpu_ctx *ctx)
+{
+    if (ctx == NULL)
+        return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream)
+        (void)hipStreamSynchronize(ctx->stream);
+    for (auto &s : ctx->seqs)
+        slot_free(s);
+    for (auto &p : ctx->pending)
+        ctx->pool.push_back(p);
+    for (auto &p : ctx->pool)
+    {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    if (ctx->d_jump)
+        (void)hipFree(ctx->d_jump);
+    if (ctx->d_counters)
+        (void)hipFree(ctx->d_counters);
+    if (ctx->h_stage)
+        (void)hipHostFree(ctx->h_stage);
+    if (ctx->stream)
+        (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+// sequence_t -> GPU template: thread_hdl() prologue, sequence.c:66-374.
+int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *seq, const uint8_t *src_mac,
+                        const uint8_t *dst_mac, const pb_rules_t *rules, uint64_t seed_base)
+{
+    if (ctx == NULL || seq == NULL || seq_idx >= PB_MAX_SEQUENCES)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    seq_slot &S = ctx->seqs[seq_idx];
+    slot_free(S);
+
+    pb_rules_t R = {PB_PAYLOAD_STREAM, PB_FOLD_FULL};
+    if (rules)
+        R = *rules;
+    if (seq->ip.dst_ip == NULL) // seq_send refuses it, sequence.c:723-728
+        return PBGPU_EINVAL;
+    if (seq->pl_cnt > PB_MAX_PAYLOADS || seq->ip.range_count > PB_MAX_RANGES)
+        return PBGPU_EINVAL;
+    if (seq->ip.min_ttl > seq->ip.max_ttl || seq->ip.min_id > seq->ip.max_id)
+        return PBGPU_EINVAL; // rand_num modulus <= 0: undefined in the reference
+
+    pb_kargs K;
+    memset(&K, 0, sizeof K);
+    uint8_t t[64];
+    memset(t, 0, sizeof t);
+
+    uint8_t sm[6], dm[6];
+    if (src_mac)
+        memcpy(sm, src_mac, 6);
+    else
+        parse_mac(seq->eth.src_mac, sm);
+    if (dst_mac)
+        memcpy(dm, dst_mac, 6);
+    else
+        parse_mac(seq->eth.dst_mac, dm);
+
+    uint32_t proto = 17;
+    if (seq->ip.protocol && str_ieq(seq->ip.protocol, "tcp"))
+        proto = 6;
+    else if (seq->ip.protocol && str_ieq(seq->ip.protocol, "icmp"))
+        proto = 1;
+    K.proto = proto;
+    K.l4len = proto == 6 ? 20 : 8;
+    K.hl = 14 + 20 + K.l4len;
+    if (proto == 17)
+        K.csum_dw = 10, K.csum_hi = 0; // byte 40
+    else if (proto == 6)
+        K.csum_dw = 12, K.csum_hi = 1; // byte 50
+    else
+        K.csum_dw = 9, K.csum_hi = 0;  // byte 36
+
+    // template, sequence.c:161-258
+    memcpy(t + 0, dm, 6);
+    memcpy(t + 6, sm, 6);
+    t[12] = 0x08;
+    t[13] = 0x00;
+    t[14] = 0x45;
+    t[15] = seq->ip.tos;
+    t[23] = (uint8_t)proto;
+    uint32_t flags = 0;
+    if (seq->ip.min_ttl != seq->ip.max_ttl)
+    {
+        flags |= PBK_RND_TTL;
+        K.ttl_min = seq->ip.min_ttl;
+        K.ttl = make_div((uint32_t)seq->ip.max_ttl - seq->ip.min_ttl + 1);
+    }
+    else
+    {
+        t[22] = seq->ip.max_ttl;
+    }
+    if (seq->ip.min_id != seq->ip.max_id)
+    {
+        flags |= PBK_RND_ID;
+        K.id_min = seq->ip.min_id;
+        K.id = make_div((uint32_t)seq->ip.max_id - seq->ip.min_id + 1);
+    }
+    else
+    {
+        t[18] = (uint8_t)(seq->ip.max_id >> 8);
+        t[19] = (uint8_t)seq->ip.max_id;
+    }
+    std::vector<uint2> ranges;
+    if (seq->ip.src_ip != NULL)
+    {
+        struct in_addr a;
+        memset(&a, 0, sizeof a);
+        inet_aton(seq->ip.src_ip, &a);
+        memcpy(t + 26, &a.s_addr, 4);
+    }
+    else if (seq->ip.range_count > 0)
+    {
+        flags |= PBK_RND_SADDR;
+        for (int r = 0; r < seq->ip.range_count; ++r)
+            ranges.push_back(compile_range(seq->ip.ranges[r]));
+        K.rng = make_div(seq->ip.range_count);
+    }
+    else
+    {
+        const uint32_t lo = htonl(0x7F000001u); // sequence.c:484-490
+        memcpy(t + 26, &lo, 4);
+    }
+    {
+        struct in_addr a;
+        memset(&a, 0, sizeof a);
+        inet_aton(seq->ip.dst_ip, &a);
+        memcpy(t + 30, &a.s_addr, 4);
+    }
+    if (proto == 17 || proto == 6)
+    {
+        const uint16_t sp = proto == 17 ? seq->udp.src_port : seq->tcp.src_port;
+        const uint16_t dp = proto == 17 ? seq->udp.dst_port : seq->tcp.dst_port;
+        if (sp)
+            t[34] = (uint8_t)(sp >> 8), t[35] = (uint8_t)sp;
+        else
+            flags |= PBK_RND_SPORT;
+        if (dp)
+            t[36] = (uint8_t)(dp >> 8), t[37] = (uint8_t)dp;
+        else
+            flags |= PBK_RND_DPORT;
+        K.port = make_div(65535);
+        flags |= PBK_PSEUDO;
+    }
+    if (proto == 6)
+    {
+        t[46] = 5 << 4;
+        t[47] = (uint8_t)((seq->tcp.fin & 1) | (seq->tcp.syn & 1) << 1 | (seq->tcp.rst & 1) << 2 |
+                          (seq->tcp.psh & 1) << 3 | (seq->tcp.ack & 1) << 4 | (seq->tcp.urg & 1) << 5 |
+                          (seq->tcp.ece & 1) << 6 | (seq->tcp.cwr & 1) << 7);
+    }
+    else if (proto == 1)
+    {
+        t[34] = seq->icmp.type;
+        t[35] = seq->icmp.code;
+    }
+    if (seq->ip.csum)
+        flags |= PBK_IP_CSUM;
+    if (seq->l4_csum)
+        flags |= PBK_L4_CSUM;
+    if (R.iph_fold == PB_FOLD_SINGLE)
+        flags |= PBK_IPH_SINGLE;
+    if (R.payload_rule == PB_PAYLOAD_LITERAL)
+        flags |= PBK_LITERAL;
+    memcpy(K.tmpl, t, 64);
+
+    // payloads, sequence.c:264-374
+    std::vector<pb_pl> pls;
+    std::vector<uint8_t> blob(16, 0);
+    uint16_t dl_setup[PB_MAX_PAYLOADS];
+    memset(dl_setup, 0, sizeof dl_setup);
+    uint32_t sseed = host_seed(seed_base, seq_idx, PB_STATIC_SEED_K); // quirk B2
+    int n_random = 0;
+    uint32_t max_random = 0;
+    for (int i = 0; i < seq->pl_cnt; ++i)
+    {
+        const pb_payload_opt_t *po = &seq->pls[i];
+        pb_pl P;
+        memset(&P, 0, sizeof P);
+        std::vector<uint8_t> bytes;
+        bool is_static = po->is_static;
+        if (po->exact != NULL)
+        {
+            is_static = true;
+            int rc = compile_exact(po, bytes);
+            if (rc)
+                return rc;
+        }
+        else if (po->is_static && po->max_len > 0)
+        {
+            if (po->min_len > po->max_len)
+                return PBGPU_EINVAL;
+            uint32_t s2 = sseed;
+            const uint32_t len = po->min_len + host_rand_r(&s2) % ((uint32_t)po->max_len - po->min_len + 1);
+            dl_setup[i] = (uint16_t)len;
+            bytes.assign(len, 0);
+            if (R.payload_rule == PB_PAYLOAD_LITERAL)
+            {
+                for (uint32_t j = 0; j < PB_MAX_PAYLOADS && j < dl_setup[j]; ++j)
+                    bytes[j] = (uint8_t)host_rand_r(&sseed);
+            }
+            else
+            {
+                for (uint32_t j = 0; j < len; ++j)
+                    bytes[j] = (uint8_t)host_rand_r(&sseed);
+            }
+        }
+        if (is_static)
+        {
+            dl_setup[i] = (uint16_t)bytes.size();
+            P.random = 0;
+            P.slen = (uint32_t)bytes.size();
+            P.blob_off = (uint32_t)blob.size();
+            P.ssum = le_word_sum(bytes.data(), bytes.size());
+            blob.insert(blob.end(), bytes.begin(), bytes.end());
+            blob.insert(blob.end(), 48 - (bytes.size() & 15), 0); // >= 32 B zero pad, 16-B aligned
+        }
+        else if (po->max_len > 0)
+        {
+            if (po->min_len > po->max_len)
+                return PBGPU_EINVAL;
+            P.random = 1;
+            P.min_len = po->min_len;
+            P.len = make_div((uint32_t)po->max_len - po->min_len + 1);
+            ++n_random;
+            if (po->max_len > max_random)
+                max_random = po->max_len;
+        }
+        else
+        {
+            P.random = 0; // non-static, max_len 0: empty payload (sequence.c:557-560)
+            P.slen = 0;
+            P.blob_off = 16;
+        }
+        if (K.hl + (P.random ? po->max_len : P.slen) > PB_MAX_PCKT_LEN)
+            return PBGPU_EINVAL;
+        pls.push_back(P);
+    }
+    if (pls.empty()) // sequence.c:364-374
+    {
+        pb_pl P;
+        memset(&P, 0, sizeof P);
+        P.blob_off = 16;
+        pls.push_back(P);
+    }
+    if ((flags & PBK_LITERAL) && pls.size() > 1 && n_random > 0)
+        return PBGPU_ENOTSUP; // history-dependent quirk (B8): oracle only
+    if ((flags & PBK_LITERAL) || max_random <= 64)
+        flags |= PBK_SUM_IN_A;
+
+    K.pl_cnt = (uint32_t)pls.size();
+    K.pl0 = pls[0];
+    K.flags = flags;
+    K.seed_base = seed_base;
+    K.seq = seq_idx;
+
+    // frame lengths
+    uint32_t minf = 0xFFFFFFFFu, maxf = 0;
+    for (const pb_pl &P : pls)
+    {
+        const uint32_t lo = K.hl + (P.random ? P.min_len : P.slen);
+        const uint32_t hi = K.hl + (P.random ? P.min_len + P.len.d - 1 : P.slen);
+        minf = lo < minf ? lo : minf;
+        maxf = hi > maxf ? hi : maxf;
+    }
+    S.min_flen = minf;
+    S.max_flen = maxf;
+    S.fpi = (uint32_t)pls.size();
+    const bool fixed = pls.size() == 1 && (!pls[0].random || pls[0].len.d == 1);
+    K.fixed_len = fixed ? minf : 0;
+    if (fixed)
+        K.flen = make_div(minf);
+    // tile: power of two, <= 16 KiB, <= (PB_NF_MAX - 2) frames of minimum length
+    uint32_t cap = (PB_NF_MAX - 2) * minf;
+    uint32_t shift = 14;
+    while (shift > 4 && (1u << shift) > cap)
+        --shift;
+    S.tile_shift = shift;
+    K.tile_bytes = 1u << shift;
+
+    int rc;
+    if ((rc = upload(&S.d_ranges, ranges.data(), ranges.size())) != PBGPU_OK)
+        return rc;
+    if ((rc = upload(&S.d_pls, pls.data(), pls.size())) != PBGPU_OK)
+        return rc;
+    blob.insert(blob.end(), 64, 0);
+    if ((rc = upload(&S.d_blob, blob.data(), blob.size())) != PBGPU_OK)
+        return rc;
+    K.ranges = S.d_ranges;
+    K.pls = S.d_pls;
+    K.blob = S.d_blob;
+    K.jump = ctx->d_jump;
+    K.counters = ctx->d_counters + 4 * seq_idx;
+    S.K = K;
+    S.loaded = true;
+    return PBGPU_OK;
+}
+
+int pbgpu_build_size(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t n_iter, uint64_t *max_frames, uint64_t *max_bytes)
+{
+    if (ctx == NULL || seq_idx >= PB_MAX_SEQUENCES)
+        return PBGPU_EINVAL;
+    const seq_slot &S = ctx->seqs[seq_idx];
+    if (!S.loaded)
+        return PBGPU_ENOENT;
+    const uint64_t nf = n_iter * S.fpi;
+    if (max_frames)
+        *max_frames = nf;
+    if (max_bytes)
+        *max_bytes = ((nf * S.max_flen + 15) & ~15ull) + 16;
+    return PBGPU_OK;
+}
+
+int pbgpu_frames_alloc(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capacity_bytes, pbgpu_frames **out)
+{
+    if (ctx == NULL || out == NULL)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    pbgpu_frames *f = (pbgpu_frames *)calloc(1, sizeof *f);
+    if (f == NULL)
+        return PBGPU_ENOMEM;
+    capacity_bytes = (capacity_bytes + 15) & ~15ull;
+    const uint64_t max_tiles = capacity_bytes / 4096 + 4; // tiles are >= 8 KiB (frames >= 42 B)
+    const uint64_t nblocks = capacity_frames / PB_SCAN_FRAMES_PER_BLOCK + 1;
+    if (hipMalloc((void **)&f->data, capacity_bytes ? capacity_bytes : 16) != hipSuccess ||
+        hipMalloc((void **)&f->offsets, (capacity_frames + 1) * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc((void **)&f->tile_first, max_tiles * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&f->scan_tmp, nblocks * sizeof(uint64_t)) != hipSuccess)
+    {
+        pbgpu_frames_free(ctx, f);
+        return PBGPU_ENOMEM;
+    }
+    f->capacity_frames = capacity_frames;
+    f->capacity_bytes = capacity_bytes;
+    f->total_bytes = 0;
+    *out = f;
+    return PBGPU_OK;
+}
+
+void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
+{
+    if (f == NULL)
+        return;
+    if (ctx)
+    {
+        (void)hipSetDevice(ctx->device);
+        (void)hipStreamSynchronize(ctx->stream);
+    }
+    if (f->data)
+        (void)hipFree(f->data);
+    if (f->offsets)
+        (void)hipFree(f->offsets);
+    if (f->tile_first)
+        (void)hipFree(f->tile_first);
+    if (f->scan_tmp)
+        (void)hipFree(f->scan_tmp);
+    free(f);
+}
+
+static int timed_pair(pbgpu_ctx *ctx, timing_pair *p)
+{
+    if (!ctx->pool.empty())
+    {
+        *p = ctx->pool.back();
+        ctx->pool.pop_back();
+        return PBGPU_OK;
+    }
+    HIPCHK(hipEventCreate(&p->a));
+    HIPCHK(hipEventCreate(&p->b));
+    return PBGPU_OK;
+}
+
+// One batch of the hot loop, sequence.c:433-602.
+int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, pbgpu_frames *out)
+{
+    if (ctx == NULL || out == NULL || seq_idx >= PB_MAX_SEQUENCES)
+        return PBGPU_EINVAL;
+    seq_slot &S = ctx->seqs[seq_idx];
+    if (!S.loaded)
+        return PBGPU_ENOENT;
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint64_t nf = n_iter * S.fpi;
+    if (nf > out->capacity_frames || nf > 0xFFFFFFFFull)
+        return PBGPU_ENOSPC;
+    if (first_iter + n_iter >= PB_STATIC_SEED_K)
+        return PBGPU_EINVAL;
+    const uint64_t max_bytes = nf * S.max_flen;
+    if (((max_bytes + 15) & ~15ull) > out->capacity_bytes)
+        return PBGPU_ENOSPC;
+
+    pb_kargs K = S.K;
+    K.first_iter = first_iter;
+    K.n_frames = nf;
+    K.out = out->data;
+    K.offsets = out->offsets;
+    K.tile_first = out->tile_first;
+    out->seq_idx = seq_idx;
+    out->first_iter = first_iter;
+    out->n_frames = nf;
+    out->fixed_len = K.fixed_len;
+    if (nf == 0)
+    {
+        out->total_bytes = 0;
+        return PBGPU_OK;
+    }
+    uint64_t n_tiles;
+    if (K.fixed_len)
+    {
+        K.total_bytes = nf * K.fixed_len;
+        out->total_bytes = K.total_bytes;
+        n_tiles = (K.total_bytes + K.tile_bytes - 1) >> S.tile_shift;
+    }
+    else
+    {
+        out->total_bytes = UINT64_MAX;
+        n_tiles = (max_bytes + K.tile_bytes - 1) >> S.tile_shift;
+        const uint64_t nblocks = (nf + PB_SCAN_FRAMES_PER_BLOCK - 1) / PB_SCAN_FRAMES_PER_BLOCK;
+        HIPCHK(pbk_launch_lengths(&K, (unsigned long long *)out->scan_tmp, (uint32_t)nblocks, out->offsets,
+                                  out->tile_first, S.tile_shift, ctx->stream));
+    }
+    if (n_tiles > 0x7FFFFFFFull)
+        return PBGPU_ENOSPC;
+    K.n_tiles = (uint32_t)n_tiles;
+    timing_pair tp;
+    int rc = timed_pair(ctx, &tp);
+    if (rc)
+        return rc;
+    HIPCHK(hipEventRecord(tp.a, ctx->stream));
+    HIPCHK(pbk_launch_build(&K, (uint32_t)n_tiles, ctx->stream));
+    HIPCHK(hipEventRecord(tp.b, ctx->stream));
+    ctx->pending.push_back(tp);
+    if (ctx->pending.size() >= 4096)
+    {
+        double ms; // bound the pending list (this drops the older timings)
+        uint32_t n;
+        rc = pbgpu_kernel_time(ctx, &ms, &n);
+        if (rc)
+            return rc;
+    }
+    return PBGPU_OK;
+}
+
+int pbgpu_sync(pbgpu_ctx *ctx)
+{
+    if (ctx == NULL)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PBGPU_OK;
+}
+
+int pbgpu_frames_total(pbgpu_ctx *ctx, pbgpu_frames *f, uint64_t *total)
+{
+    if (ctx == NULL || f == NULL)
+        return PBGPU_EINVAL;
+    if (f->fixed_len || f->n_frames == 0)
+    {
+        if (total)
+            *total = f->total_bytes;
+        return PBGPU_OK;
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    uint64_t t = 0;
+    HIPCHK(hipMemcpyAsync(&t, f->offsets + f->n_frames, sizeof t, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    f->total_bytes = t;
+    if (total)
+        *total = t;
+    return PBGPU_OK;
+}
+
+int pbgpu_copy_packed(pbgpu_ctx *ctx, const pbgpu_frames *f, void *dst, uint64_t byte_offset, uint64_t nbytes)
+{
+    if (ctx == NULL || f == NULL || dst == NULL || byte_offset + nbytes > f->capacity_bytes)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(dst, f->data + byte_offset, nbytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PBGPU_OK;
+}
+
+int pbgpu_copy_offsets(pbgpu_ctx *ctx, const pbgpu_frames *f, uint64_t *dst)
+{
+    if (ctx == NULL || f == NULL || dst == NULL)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (f->fixed_len)
+    {
+        for (uint64_t i = 0; i <= f->n_frames; ++i)
+            dst[i] = i * f->fixed_len;
+        return PBGPU_OK;
+    }
+    HIPCHK(hipMemcpyAsync(dst, f->offsets, (f->n_frames + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PBGPU_OK;
+}
+
+int pbgpu_host_register(pbgpu_ctx *ctx, void *ptr, size_t bytes)
+{
+    if (ctx == NULL || ptr == NULL)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+    return PBGPU_OK;
+}
+
+int pbgpu_host_unregister(pbgpu_ctx *ctx, void *ptr)
+{
+    if (ctx == NULL || ptr == NULL)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipHostUnregister(ptr));
+    return PBGPU_OK;
+}
+
+// send_packet()'s memcpy into UMEM slot idx * FRAME_SIZE, af_xdp.c:200-214
+int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32_t slot_stride, uint32_t first_slot,
+                       uint64_t first_frame, uint32_t n, uint16_t *lens_out)
+{
+    if (ctx == NULL || f == NULL || umem == NULL || slot_stride == 0 || first_frame + n > f->n_frames)
+        return PBGPU_EINVAL;
+    if (n == 0)
+        return PBGPU_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    uint8_t *dst = (uint8_t *)umem + (uint64_t)first_slot * slot_stride;
+    if (f->fixed_len)
+    {
+        if (f->fixed_len > slot_stride)
+            return PBGPU_EINVAL;
+        HIPCHK(hipMemcpy2DAsync(dst, slot_stride, f->data + first_frame * f->fixed_len, f->fixed_len, f->fixed_len,
+                                n, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        if (lens_out)
+            for (uint32_t i = 0; i < n; ++i)
+                lens_out[i] = (uint16_t)f->fixed_len;
+        return PBGPU_OK;
+    }
+    // variable length: a scatter kernel writes straight into registered
+    // (mapped) UMEM; unregistered memory goes through a pinned staging copy.
+    void *dev_dst = NULL;
+    uint16_t *d_lens = NULL;
+    if (hipHostGetDevicePointer(&dev_dst, dst, 0) == hipSuccess && dev_dst != NULL)
+    {
+        HIPCHK(hipMallocAsync((void **)&d_lens, (size_t)n * 2, ctx->stream));
+        HIPCHK(pbk_launch_scatter(f->data, f->offsets, first_frame, n, (uint8_t *)dev_dst, slot_stride, d_lens,
+                                  ctx->stream));
+        if (lens_out)
+            HIPCHK(hipMemcpyAsync(lens_out, d_lens, (size_t)n * 2, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipFreeAsync(d_lens, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        return PBGPU_OK;
+    }
+    (void)hipGetLastError();
+    std::vector<uint64_t> off(n + 1);
+    HIPCHK(hipMemcpyAsync(off.data(), f->offsets + first_frame, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    const uint64_t bytes = off[n] - off[0];
+    if (ctx->h_stage_bytes < bytes)
+    {
+        if (ctx->h_stage)
+            (void)hipHostFree(ctx->h_stage);
+        ctx->h_stage = NULL;
+        ctx->h_stage_bytes = 0;
+        HIPCHK(hipHostMalloc((void **)&ctx->h_stage, bytes, 0));
+        ctx->h_stage_bytes = bytes;
+    }
+    HIPCHK(hipMemcpyAsync(ctx->h_stage, f->data + off[0], bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        const uint64_t len = off[i + 1] - off[i];
+        if (len > slot_stride)
+            return PBGPU_EINVAL;
+        memcpy(dst + (uint64_t)i * slot_stride, ctx->h_stage + (off[i] - off[0]), len);
+        if (lens_out)
+            lens_out[i] = (uint16_t)len;
+    }
+    return PBGPU_OK;
+}
+
+int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)
+{
+    if (ctx == NULL || n_seq < 0 || n_seq > PB_MAX_SEQUENCES)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    std::vector<unsigned long long> h(4 * (size_t)PB_MAX_SEQUENCES);
+    HIPCHK(hipMemcpyAsync(h.data(), ctx->d_counters, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    int bad = 0;
+    for (int i = 0; i < n_seq; ++i)
+    {
+        if (pckts)
+            pckts[i] = h[4 * i + 0];
+        if (bytes)
+            bytes[i] = h[4 * i + 1];
+        bad |= h[4 * i + 2] != 0;
+    }
+    return bad ? PBGPU_EIO : PBGPU_OK;
+}
+
+int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches)
+{
+    if (ctx == NULL)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    double tot = 0;
+    uint32_t n = 0;
+    for (auto &p : ctx->pending)
+    {
+        HIPCHK(hipEventSynchronize(p.b));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+        tot += ms;
+        ++n;
+        ctx->pool.push_back(p);
+    }
+    ctx->pending.clear();
+    if (ms_total)
+        *ms_total = tot;
+    if (n_launches)
+        *n_launches = n;
+    return PBGPU_OK;
+}
+
+int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_launch)
+{
+    if (ctx == NULL || bytes < 16 || reps == 0)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    void *buf = NULL;
+    HIPCHK(hipMalloc(&buf, bytes));
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(pbk_launch_fill(buf, bytes, ctx->stream)); // warm-up
+    HIPCHK(hipEventRecord(a, ctx->stream));
+    for (uint32_t r = 0; r < reps; ++r)
+        HIPCHK(pbk_launch_fill(buf, bytes, ctx->stream));
+    HIPCHK(hipEventRecord(b, ctx->stream));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipFree(buf);
+    if (ms_per_launch)
+        *ms_per_launch = ms / reps;
+    return PBGPU_OK;
+}
+
+int pbgpu_tile_bytes(pbgpu_ctx *ctx, uint16_t seq_idx, uint32_t *tile_bytes)
+{
+    if (ctx == NULL || seq_idx >= PB_MAX_SEQUENCES || tile_bytes == NULL)
+        return PBGPU_EINVAL;
+    if (!ctx->seqs[seq_idx].loaded)
+        return PBGPU_ENOENT;
+    *tile_bytes = ctx->seqs[seq_idx].K.tile_bytes;
+    return PBGPU_OK;
+}
+
+size_t pbgpu_abi_size(int which)
+{
+    switch (which)
+    {
+    case 0: return sizeof(pb_sequence_t);
+    case 1: return sizeof(pb_payload_opt_t);
+    case 2: return sizeof(pbgpu_frames);
+    case 3: return offsetof(pb_sequence_t, ip.ranges);
+    case 4: return offsetof(pb_sequence_t, pls);
+    case 5: return offsetof(pb_sequence_t, pl_cnt);
+    case 6: return offsetof(pbgpu_frames, total_bytes);
+    default: return 0;
+    }
+}
+
+} // extern "C"

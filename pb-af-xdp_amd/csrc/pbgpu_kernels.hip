@@ -1,0 +1,634 @@
+// pbgpu_kernels.hip — MI355X (gfx950) frame-build kernels.
+//
+// Hot path: PB-AF-XDP thread_hdl() loop body, src/sequence.c:433-602, for a
+// batch of iterations at once.  One workgroup owns one TILE of the packed
+// output stream (a power-of-two byte range, <= 16 KiB) and writes every
+// 16-B chunk of it exactly once with an aligned non-temporal dwordx4 store,
+// whatever the frame lengths and alignments are:
+//
+//   phase A  one lane per frame touching the tile: seed -> r0 -> TTL / ID /
+//            source IP / ports / payload length (sequence.c:434-527, 548),
+//            header image (sequence.c:150-258) with IPv4 checksum
+//            (sequence.c:596-602) into LDS, L4 header + pseudo-header sum.
+//   phase B  one lane per 16-B chunk: payload bytes (glibc rand_r low byte,
+//            sequence.c:552-555) generated directly in output alignment with
+//            a jump table + 24-bit LCG steps; per-frame payload word sums
+//            accumulated in LDS (csum_partial, sequence.c:572/581/590).
+//            Payload that spills past the tile is summed (not stored) so the
+//            tile that holds a frame's checksum field can finish it.
+//   phase C  one lane per frame: fold + complement the L4 checksum into the
+//            header image (csum_tcpudp_magic / icmp_csum).
+//   phase D  one lane per chunk: OR the header bytes of the (at most two)
+//            frames overlapping the chunk into its payload bytes, store.
+//
+// The template, CIDR table pointers and divisors arrive as kernel arguments
+// (scalar registers); header images, per-frame records and the chunk->frame
+// map live in LDS.  No inter-workgroup communication; no atomics to HBM
+// except two counter adds per launch.
+#include "pb_device.h"
+
+#define PB_IMG_STRIDE 20   // dwords per frame image row (16 used + pad: conflict-free b128 rows)
+#define PB_SCAN_ITEMS 8    // frames per thread in the length scan kernels
+
+typedef uint32_t pb_u32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+struct pb_frame_pl
+{
+    uint32_t random;
+    uint32_t plen;
+    uint32_t nvalid;   // random bytes actually drawn (literal rule: <= 1)
+    uint32_t st0;      // LCG state entering the payload (random)
+    uint32_t blob_off; // static
+    uint32_t ssum;     // static word sum (folded)
+};
+
+// L^(3 n)(s): the seed after n rand_r calls.
+__device__ __forceinline__ uint32_t pb_jump(const pb_kargs &K, uint32_t s, uint32_t n)
+{
+    if (n == 0)
+        return s;
+    const uint2 t = K.jump[n - 1 + PB_JNEG];
+    return t.x * s + t.y;
+}
+
+// Payload i of an iteration whose seed is s (sequence.c:529-561).
+__device__ __forceinline__ pb_frame_pl pb_payload(const pb_kargs &K, uint32_t s, uint32_t i)
+{
+    pb_pl P;
+    uint32_t cur = s;
+    if (K.pl_cnt == 1)
+    {
+        P = K.pl0;
+    }
+    else
+    {
+        // earlier random payloads advance the seed by one rand_r per byte
+        for (uint32_t p = 0; p < i; ++p)
+        {
+            const pb_pl Q = K.pls[p];
+            if (Q.random)
+            {
+                const uint32_t len = Q.min_len + pb_mod(pb_rand_r(cur), Q.len);
+                cur = pb_jump(K, cur, len);
+            }
+        }
+        P = K.pls[i];
+    }
+    pb_frame_pl r;
+    if (P.random)
+    {
+        r.random = 1;
+        r.plen = P.min_len + pb_mod(pb_rand_r(cur), P.len);
+        r.nvalid = (K.flags & PBK_LITERAL) ? min(r.plen, 1u) : r.plen;
+        r.st0 = cur;
+        r.blob_off = 0;
+        r.ssum = 0;
+    }
+    else
+    {
+        r.random = 0;
+        r.plen = P.slen;
+        r.nvalid = P.slen;
+        r.st0 = 0;
+        r.blob_off = P.blob_off;
+        r.ssum = P.ssum;
+    }
+    return r;
+}
+
+__device__ __forceinline__ void pb_frame_index(const pb_kargs &K, uint64_t f, uint64_t &k, uint32_t &i)
+{
+    if (K.pl_cnt == 1)
+    {
+        k = f;
+        i = 0;
+    }
+    else
+    {
+        k = f / K.pl_cnt;
+        i = (uint32_t)(f - k * K.pl_cnt);
+    }
+}
+
+__device__ __forceinline__ uint32_t pb_frame_len(const pb_kargs &K, uint64_t f)
+{
+    uint64_t k;
+    uint32_t i;
+    pb_frame_index(K, f, k, i);
+    const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+    return K.hl + pb_payload(K, s, i).plen;
+}
+
+// keep bytes [lo, hi) of dword t (byte positions 4t .. 4t+3)
+__device__ __forceinline__ uint32_t pb_bytemask(int lo, int hi, int t)
+{
+    const int a = lo - 4 * t;
+    const int b = hi - 4 * t;
+    const uint32_t ge = a <= 0 ? 0xFFFFFFFFu : (a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a)));
+    const uint32_t lt = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * b)));
+    return ge & lt;
+}
+
+// 4 payload bytes from 4 consecutive LCG states: byte = state[23:16]
+__device__ __forceinline__ uint32_t pb_pack4(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3)
+{
+    const uint32_t lo = __builtin_amdgcn_perm(x1, x0, 0x0C0C0602u);
+    const uint32_t hi = __builtin_amdgcn_perm(x3, x2, 0x0C0C0602u);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+// 24-bit LCG step: three rand_r steps folded into one affine map mod 2^24.
+__device__ __forceinline__ uint32_t pb_step3(uint32_t x, uint32_t a3, uint32_t c3)
+{
+    return __umul24(x, a3) + c3;
+}
+
+// 4 bytes of a frame-local header image starting at byte x (x may be < 0;
+// bytes outside [0, 4 * PB_IMG_STRIDE) read as zero).
+__device__ __forceinline__ uint32_t pb_window(const uint32_t *img, int x)
+{
+    const int i0 = x >> 2; // floor
+    const uint32_t sh = (uint32_t)x & 3u;
+    const uint32_t lo = (i0 >= 0) ? img[i0] : 0u;
+    const uint32_t hi = (i0 + 1 >= 0) ? img[i0 + 1] : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+} // namespace
+
+// One payload byte = three glibc LCG steps: x -> A3 * x + C3 (mod 2^32).
+constexpr uint32_t PB_A3 = PB_LCG_A * PB_LCG_A * PB_LCG_A;
+constexpr uint32_t PB_C3 = PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u);
+
+template <bool FIXED>
+__global__ __launch_bounds__(PB_WG) void pb_build_kernel(pb_kargs K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_img[PB_NF_MAX * PB_IMG_STRIDE];
+    __shared__ int32_t s_rel[PB_NF_MAX];     // frame offset relative to tile start
+    __shared__ uint32_t s_nv[PB_NF_MAX];     // nvalid | random << 31
+    __shared__ uint32_t s_src[PB_NF_MAX];    // st0 (random) or blob_off (static)
+    __shared__ uint32_t s_hsum[PB_NF_MAX];   // L4 header + pseudo header + frame-aligned payload sum
+    __shared__ uint32_t s_psc[PB_NF_MAX];    // payload sum from chunks (output alignment)
+    __shared__ uint16_t s_map[FIXED ? 1 : PB_TILE_MAX / 16]; // chunk -> frame holding its first byte
+    __shared__ uint32_t s_nvirt, s_vframe;
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t flags = K.flags;
+    const uint64_t tile_start = (uint64_t)tile * K.tile_bytes;
+    const uint64_t total = FIXED ? K.total_bytes : K.offsets[K.n_frames];
+    if (tile_start >= total)
+        return; // variable length: grid sized for the upper bound
+    const uint32_t tile_len = (uint32_t)min((uint64_t)K.tile_bytes, total - tile_start);
+    const uint32_t nchunks = (tile_len + 15u) >> 4;
+
+    uint64_t fa, fb;
+    if (FIXED)
+    {
+        fa = tile_start / K.fixed_len;
+        fb = (tile_start + tile_len - 1) / K.fixed_len;
+    }
+    else
+    {
+        fa = K.tile_first[tile];
+        fb = K.tile_first[tile + 1];
+    }
+    uint32_t nf = (uint32_t)(fb - fa + 1);
+    if (nf > PB_NF_MAX)
+    {
+        if (tid == 0)
+            atomicAdd(K.counters + 2, 1ull); // host sizing bug: flagged, never silent
+        nf = PB_NF_MAX;
+    }
+
+    if (tid == 0)
+    {
+        s_nvirt = 0;
+        s_vframe = 0;
+    }
+
+    // ---------------- phase A: one lane per frame ----------------
+    for (uint32_t lf = tid; lf < nf; lf += PB_WG)
+    {
+        const uint64_t f = fa + lf;
+        uint64_t off;
+        uint32_t flen;
+        if (FIXED)
+        {
+            off = f * K.fixed_len;
+            flen = K.fixed_len;
+        }
+        else
+        {
+            off = K.offsets[f];
+            flen = (uint32_t)(K.offsets[f + 1] - off);
+        }
+        const int32_t rel = (int32_t)((int64_t)off - (int64_t)tile_start);
+
+        uint64_t k;
+        uint32_t pi;
+        pb_frame_index(K, f, k, pi);
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+        const uint32_t r0 = pb_rand_r(s);
+        const pb_frame_pl P = pb_payload(K, s, pi);
+
+        uint32_t d[16];
+#pragma unroll
+        for (int w = 0; w < 16; ++w)
+            d[w] = K.tmpl[w];
+
+        if (flags & PBK_RND_TTL) // sequence.c:443-446
+            d[5] |= ((K.ttl_min + pb_mod(r0, K.ttl)) & 0xFFu) << 16;
+        if (flags & PBK_RND_ID) // sequence.c:449-452
+            d[4] |= pb_bswap16((K.id_min + pb_mod(r0, K.id)) & 0xFFFFu) << 16;
+        if (flags & PBK_RND_SADDR) // sequence.c:455-497
+        {
+            const uint2 rg = K.ranges[pb_mod(r0, K.rng)];
+            const uint32_t sa = __builtin_bswap32(rg.x | (r0 & rg.y));
+            d[6] |= sa << 16;
+            d[7] |= sa >> 16;
+        }
+        if (flags & (PBK_RND_SPORT | PBK_RND_DPORT)) // sequence.c:500-527
+        {
+            const uint32_t port = pb_bswap16(1u + pb_mod(r0, K.port));
+            if (flags & PBK_RND_SPORT)
+                d[8] |= port << 16;
+            if (flags & PBK_RND_DPORT)
+                d[9] |= port;
+        }
+        const uint32_t l4tot = K.l4len + P.plen;
+        d[4] |= pb_bswap16(20u + l4tot); // tot_len, sequence.c:597
+        if (K.proto == 17u)
+            d[9] |= pb_bswap16(l4tot) << 16; // udph->len, sequence.c:567
+
+        if (flags & PBK_IP_CSUM) // update_iph_checksum, sequence.c:599-602
+        {
+            const uint32_t sum = (d[3] >> 16) + pb_halves(d[4]) + pb_halves(d[5]) + (d[6] >> 16) +
+                                 pb_halves(d[7]) + (d[8] & 0xFFFFu);
+            const uint32_t c = (flags & PBK_IPH_SINGLE) ? ~((sum & 0xFFFFu) + (sum >> 16)) : ~pb_fold(sum);
+            d[6] |= c & 0xFFFFu;
+        }
+
+        // L4 header words (check field still 0) + pseudo header
+        uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) +
+                      pb_halves(d[12]) + pb_halves(d[13]);
+        if (flags & PBK_PSEUDO)
+            hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
+        if (!P.random)
+        {
+            hs += P.ssum;
+        }
+        else if (flags & PBK_SUM_IN_A)
+        {
+            uint32_t x = P.st0;
+            uint32_t ps = 0;
+            for (uint32_t j = 0; j < P.nvalid; ++j)
+            {
+                x = x * PB_LCG_A + PB_LCG_C;
+                x = x * PB_LCG_A + PB_LCG_C;
+                x = x * PB_LCG_A + PB_LCG_C;
+                ps += ((x >> 16) & 0xFFu) << ((j & 1u) << 3);
+            }
+            hs += ps;
+        }
+
+        uint4 *row = reinterpret_cast<uint4 *>(s_img + lf * PB_IMG_STRIDE);
+        row[0] = make_uint4(d[0], d[1], d[2], d[3]);
+        row[1] = make_uint4(d[4], d[5], d[6], d[7]);
+        row[2] = make_uint4(d[8], d[9], d[10], d[11]);
+        row[3] = make_uint4(d[12], d[13], d[14], d[15]);
+        row[4] = make_uint4(0u, 0u, 0u, 0u);
+        s_rel[lf] = rel;
+        s_nv[lf] = P.nvalid | (P.random << 31);
+        s_src[lf] = P.random ? P.st0 : P.blob_off;
+        s_hsum[lf] = hs;
+        s_psc[lf] = 0;
+
+        if (!FIXED)
+        {
+            int32_t c0 = rel <= 0 ? 0 : (rel + 15) >> 4;
+            int32_t c1 = (rel + (int32_t)flen - 1) >> 4;
+            if (c1 >= (int32_t)nchunks)
+                c1 = (int32_t)nchunks - 1;
+            for (int32_t c = c0; c <= c1; ++c)
+                s_map[c] = (uint16_t)lf;
+        }
+
+        // payload past the tile end of a frame whose checksum field is in this tile
+        if ((flags & PBK_L4_CSUM) && P.random && !(flags & PBK_SUM_IN_A))
+        {
+            const int32_t cpos = rel + (int32_t)(K.csum_dw * 4 + K.csum_hi * 2);
+            const int32_t span = (int32_t)(nchunks * 16);
+            if (cpos >= 0 && cpos < (int32_t)tile_len && rel + (int32_t)flen > span)
+            {
+                s_nvirt = (uint32_t)((rel + (int32_t)flen - span + 15) >> 4);
+                s_vframe = lf;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---------------- phase B: payload bytes per 16-B chunk ----------------
+    const uint32_t a3 = PB_A3, c3 = PB_C3;
+    const bool chunk_sums = (flags & PBK_L4_CSUM) && !(flags & PBK_SUM_IN_A);
+    const int32_t hl = (int32_t)K.hl;
+
+    auto gen = [&](uint32_t a, int32_t pos, uint32_t (&o)[4]) {
+        o[0] = o[1] = o[2] = o[3] = 0u;
+        const int32_t rel = s_rel[a];
+        const uint32_t nv = s_nv[a];
+        const int32_t nvalid = (int32_t)(nv & 0x7FFFFFFFu);
+        const int32_t j0 = pos - rel - hl; // payload index of the chunk's first byte
+        if (j0 >= nvalid || j0 + 16 <= 0)
+            return;
+        const int lo = j0 < 0 ? -j0 : 0;
+        const int hi = (nvalid - j0) < 16 ? (nvalid - j0) : 16;
+        if (nv >> 31)
+        {
+            const uint2 jt = K.jump[j0 + PB_JNEG];
+            uint32_t x0 = jt.x * s_src[a] + jt.y;
+            uint32_t x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+            o[0] = pb_pack4(x0, x1, x2, x3);
+            x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+            o[1] = pb_pack4(x0, x1, x2, x3);
+            x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+            o[2] = pb_pack4(x0, x1, x2, x3);
+            x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+            o[3] = pb_pack4(x0, x1, x2, x3);
+        }
+        else
+        {
+            const uint8_t *b = K.blob + s_src[a] + j0;
+            const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)b & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)((uintptr_t)b & 3);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+            o[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            o[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            o[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+            o[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+        }
+        if (lo > 0 || hi < 16)
+        {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                o[t] &= pb_bytemask(lo, hi, t);
+        }
+        if (chunk_sums && (nv >> 31))
+        {
+            const uint32_t sum = pb_halves(o[0]) + pb_halves(o[1]) + pb_halves(o[2]) + pb_halves(o[3]);
+            atomicAdd(&s_psc[a], sum);
+        }
+    };
+
+    uint32_t data[PB_CPL][4];
+    uint32_t fr[PB_CPL];
+    const int32_t rel0 = s_rel[0];
+#pragma unroll
+    for (int ci = 0; ci < PB_CPL; ++ci)
+    {
+        const uint32_t c = tid + ci * PB_WG;
+        data[ci][0] = data[ci][1] = data[ci][2] = data[ci][3] = 0u;
+        fr[ci] = 0;
+        if (c < nchunks)
+        {
+            const uint32_t a = FIXED ? pb_divq((uint32_t)((int32_t)(c * 16) - rel0), K.flen) : (uint32_t)s_map[c];
+            fr[ci] = a;
+            gen(a, (int32_t)(c * 16), data[ci]);
+        }
+    }
+    {
+        const uint32_t nvirt = s_nvirt;
+        const uint32_t vf = s_vframe;
+        for (uint32_t v = tid; v < nvirt; v += PB_WG)
+        {
+            uint32_t tmp[4];
+            gen(vf, (int32_t)((nchunks + v) * 16), tmp);
+        }
+    }
+    __syncthreads();
+
+    // ---------------- phase C: finish L4 checksums ----------------
+    if (flags & PBK_L4_CSUM)
+    {
+        for (uint32_t lf = tid; lf < nf; lf += PB_WG)
+        {
+            uint32_t pc = pb_fold(s_psc[lf]);
+            if (s_rel[lf] & 1) // chunk sums were taken in output alignment
+                pc = pb_bswap16(pc);
+            const uint32_t c = (~pb_fold(pb_fold(s_hsum[lf]) + pc)) & 0xFFFFu;
+            s_img[lf * PB_IMG_STRIDE + K.csum_dw] |= K.csum_hi ? (c << 16) : c;
+        }
+    }
+    __syncthreads();
+
+    // ---------------- phase D: merge header bytes, store ----------------
+    uint8_t *const out = K.out + tile_start;
+#pragma unroll
+    for (int ci = 0; ci < PB_CPL; ++ci)
+    {
+        const uint32_t c = tid + ci * PB_WG;
+        if (c < nchunks)
+        {
+            const uint32_t a = fr[ci];
+            const int32_t pos = (int32_t)(c * 16);
+            const int32_t qc = pos - s_rel[a];
+            uint32_t o0 = data[ci][0], o1 = data[ci][1], o2 = data[ci][2], o3 = data[ci][3];
+            if (qc < hl)
+            {
+                const uint32_t *img = s_img + a * PB_IMG_STRIDE;
+                o0 |= pb_window(img, qc);
+                o1 |= pb_window(img, qc + 4);
+                o2 |= pb_window(img, qc + 8);
+                o3 |= pb_window(img, qc + 12);
+            }
+            if (a + 1 < nf)
+            {
+                const int32_t relb = s_rel[a + 1];
+                if (relb < pos + 16)
+                {
+                    const uint32_t *img = s_img + (a + 1) * PB_IMG_STRIDE;
+                    const int32_t xb = pos - relb;
+                    o0 |= pb_window(img, xb);
+                    o1 |= pb_window(img, xb + 4);
+                    o2 |= pb_window(img, xb + 8);
+                    o3 |= pb_window(img, xb + 12);
+                }
+            }
+            __builtin_nontemporal_store(pb_u32x4{o0, o1, o2, o3}, reinterpret_cast<pb_u32x4 *>(out + pos));
+        }
+    }
+
+    if (FIXED && tile == 0 && tid == 0)
+    {
+        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
+        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+    }
+}
+
+// ---------------- variable length: lengths -> offsets -> tile map ----------------
+
+__global__ __launch_bounds__(256) void pb_len_reduce(pb_kargs K, unsigned long long *block_sums)
+{
+    __shared__ unsigned long long s_part[256];
+    const uint64_t base = (uint64_t)blockIdx.x * 256 * PB_SCAN_ITEMS + (uint64_t)threadIdx.x * PB_SCAN_ITEMS;
+    unsigned long long sum = 0;
+    for (int it = 0; it < PB_SCAN_ITEMS; ++it)
+    {
+        const uint64_t f = base + it;
+        if (f < K.n_frames)
+            sum += pb_frame_len(K, f);
+    }
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t w = 128; w > 0; w >>= 1)
+    {
+        if (threadIdx.x < w)
+            s_part[threadIdx.x] += s_part[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        block_sums[blockIdx.x] = s_part[0];
+}
+
+// single workgroup: exclusive scan of the block sums in place
+__global__ __launch_bounds__(1024) void pb_scan_blocks(unsigned long long *block_sums, uint32_t nblocks,
+                                                       uint64_t *offsets, uint64_t n_frames,
+                                                       unsigned long long *counters)
+{
+    __shared__ unsigned long long s_v[1024];
+    unsigned long long carry = 0;
+    for (uint32_t base = 0; base < nblocks; base += 1024)
+    {
+        const uint32_t i = base + threadIdx.x;
+        const unsigned long long v = i < nblocks ? block_sums[i] : 0ull;
+        s_v[threadIdx.x] = v;
+        __syncthreads();
+        for (uint32_t d = 1; d < 1024; d <<= 1)
+        {
+            const unsigned long long t = threadIdx.x >= d ? s_v[threadIdx.x - d] : 0ull;
+            __syncthreads();
+            s_v[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (i < nblocks)
+            block_sums[i] = carry + s_v[threadIdx.x] - v;
+        const unsigned long long tot = s_v[1023];
+        __syncthreads();
+        carry += tot;
+    }
+    if (threadIdx.x == 0)
+    {
+        offsets[n_frames] = carry;
+        atomicAdd(counters + 0, (unsigned long long)n_frames);
+        atomicAdd(counters + 1, carry);
+    }
+}
+
+__global__ __launch_bounds__(256) void pb_len_scan(pb_kargs K, const unsigned long long *block_sums,
+                                                   uint64_t *offsets, uint32_t *tile_first, uint32_t tile_shift)
+{
+    __shared__ unsigned long long s_v[256];
+    const uint64_t base = (uint64_t)blockIdx.x * 256 * PB_SCAN_ITEMS + (uint64_t)threadIdx.x * PB_SCAN_ITEMS;
+    uint32_t len[PB_SCAN_ITEMS];
+    unsigned long long sum = 0;
+#pragma unroll
+    for (int it = 0; it < PB_SCAN_ITEMS; ++it)
+    {
+        const uint64_t f = base + it;
+        len[it] = f < K.n_frames ? pb_frame_len(K, f) : 0u;
+        sum += len[it];
+    }
+    s_v[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1)
+    {
+        const unsigned long long t = threadIdx.x >= d ? s_v[threadIdx.x - d] : 0ull;
+        __syncthreads();
+        s_v[threadIdx.x] += t;
+        __syncthreads();
+    }
+    unsigned long long off = block_sums[blockIdx.x] + s_v[threadIdx.x] - sum;
+#pragma unroll
+    for (int it = 0; it < PB_SCAN_ITEMS; ++it)
+    {
+        const uint64_t f = base + it;
+        if (f < K.n_frames)
+        {
+            offsets[f] = off;
+            // tiles whose first byte lies in this frame
+            const uint64_t tmask = (1ull << tile_shift) - 1;
+            const uint64_t t0 = (off + tmask) >> tile_shift;
+            const uint64_t t1 = (off + len[it] - 1) >> tile_shift;
+            for (uint64_t t = t0; t <= t1; ++t)
+                tile_first[t] = (uint32_t)f;
+            if (f == K.n_frames - 1)
+                tile_first[t1 + 1] = (uint32_t)f; // sentinel: fb of the last tile
+            off += len[it];
+        }
+    }
+}
+
+// ---------------- UMEM landing (variable length) and roofline probe ----------------
+
+// frame first + blockIdx.x -> dst + slot * stride (mapped host memory or device)
+__global__ __launch_bounds__(64) void pb_scatter_slots(const uint8_t *src, const uint64_t *offsets, uint64_t first,
+                                                       uint8_t *dst, uint32_t stride, uint16_t *lens)
+{
+    const uint64_t f = first + blockIdx.x;
+    const uint64_t o = offsets[f];
+    const uint32_t len = (uint32_t)(offsets[f + 1] - o);
+    if (threadIdx.x == 0)
+        lens[blockIdx.x] = (uint16_t)len;
+    const uint8_t *s = src + o;
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst + (uint64_t)blockIdx.x * stride);
+    const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)s & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
+    for (uint32_t i = threadIdx.x; i * 4 < len; i += 64)
+        d[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+}
+
+__global__ __launch_bounds__(256) void pb_fill_kernel(pb_u32x4 *dst, uint64_t n16, uint32_t v)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+        __builtin_nontemporal_store(pb_u32x4{v, v ^ (uint32_t)i, v, (uint32_t)i}, dst + i);
+}
+
+// ---------------- launch wrappers (called from pbgpu.cpp) ----------------
+
+extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid, hipStream_t st)
+{
+    if (K->fixed_len)
+        hipLaunchKernelGGL(pb_build_kernel<true>, dim3(n_tiles_grid), dim3(PB_WG), 0, st, *K);
+    else
+        hipLaunchKernelGGL(pb_build_kernel<false>, dim3(n_tiles_grid), dim3(PB_WG), 0, st, *K);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
+                                         uint64_t *offsets, uint32_t *tile_first, uint32_t tile_shift,
+                                         hipStream_t st)
+{
+    hipLaunchKernelGGL(pb_len_reduce, dim3(nblocks), dim3(256), 0, st, *K, block_sums);
+    hipLaunchKernelGGL(pb_scan_blocks, dim3(1), dim3(1024), 0, st, block_sums, nblocks, offsets, K->n_frames,
+                       K->counters);
+    hipLaunchKernelGGL(pb_len_scan, dim3(nblocks), dim3(256), 0, st, *K, (const unsigned long long *)block_sums,
+                       offsets, tile_first, tile_shift);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *offsets, uint64_t first, uint32_t n,
+                                         uint8_t *dst, uint32_t stride, uint16_t *lens, hipStream_t st)
+{
+    hipLaunchKernelGGL(pb_scatter_slots, dim3(n), dim3(64), 0, st, src, offsets, first, dst, stride, lens);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, hipStream_t st)
+{
+    const uint64_t n16 = bytes / 16;
+    hipLaunchKernelGGL(pb_fill_kernel, dim3(256 * 8), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+    return hipGetLastError();
+}

@@ -1,0 +1,215 @@
+"""GPU parity: libpbgpu.so (the HIP kernels, through the C ABI) against the
+committed golden vectors and the CPU oracle, bit-exact; full-size properties
+at BASELINE.json sizes.  Run on the MI355X box: pytest -m gpu."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+import pb_configs as pc
+import pbgpu
+import pyverify as pv
+from pbgpu import GpuContext, Sequence
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+INDEX = json.load(open(os.path.join(GOLD, "index.json")))["fixtures"]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = GpuContext(0)
+    yield c
+    c.close()
+
+
+def gpu_build(ctx, cfg, first, n, seq_idx=0, rule=0, fold=0, seed_base=pc.SEED_BASE):
+    seq = Sequence.from_config(cfg)
+    ctx.load_sequence(seq_idx, seq, seed_base, payload_rule=rule, iph_fold=fold)
+    mf, mb = ctx.build_size(seq_idx, n)
+    fb = ctx.alloc_frames(mf, mb)
+    ctx.build(seq_idx, first, n, fb)
+    ctx.sync()
+    data, off = fb.packed(), fb.offsets()
+    fb.free()
+    return data, off
+
+
+@pytest.mark.parametrize("fx", INDEX, ids=[f["file"] for f in INDEX])
+def test_gpu_matches_golden(ctx, fx):
+    z = np.load(os.path.join(GOLD, fx["file"]), allow_pickle=False)
+    data, off = gpu_build(ctx, pc.get(fx["config"]), fx["first_iter"], fx["n_iter"], fx["seq_idx"],
+                          fx["payload_rule"], fx["iph_fold"], fx["seed_base"])
+    assert np.array_equal(off, z["offsets"])
+    assert np.array_equal(data, z["data"])
+
+
+def _window_iters(cfg):
+    mx = 54 + max([p.get("length", {}).get("max", 0) for p in cfg.get("payloads", [])] + [256])
+    return max(64, min(40000, (24 << 20) // mx))
+
+
+CASES = [(n, 0, 0) for n in pc.ALL] + list(pc.RULE_CASES)
+
+
+@pytest.mark.parametrize("name,rule,fold", CASES)
+def test_gpu_matches_oracle(ctx, name, rule, fold):
+    """Thousands of iterations per config at an odd first_iter: every byte equal."""
+    cfg = pc.get(name)
+    n = _window_iters(cfg)
+    first = 987654321
+    g_data, g_off = gpu_build(ctx, cfg, first, n, 3, rule, fold)
+    o_data, o_off = ob.build(Sequence.from_config(cfg), 3, first, n, pc.SEED_BASE, payload_rule=rule,
+                             iph_fold=fold)
+    assert np.array_equal(g_off, o_off)
+    if not np.array_equal(g_data, o_data):
+        bad = int(np.nonzero(g_data != o_data)[0][0])
+        f = int(np.searchsorted(o_off, bad, side="right") - 1)
+        pytest.fail(f"{name}: first mismatch at byte {bad} (frame {f}, offset {bad - int(o_off[f])})")
+
+
+def test_sharded_builds_concatenate(ctx):
+    """The multi-GPU invariant: any split of the iteration range builds the
+    same frames (seeds depend only on (seq, k))."""
+    for name in ("c2_udp_64", "c3_udp_var", "c4_tcp_syn", "udp_multi_payload"):
+        cfg = pc.get(name)
+        whole, woff = gpu_build(ctx, cfg, 5000, 3000)
+        parts = [gpu_build(ctx, cfg, 5000 + a, b - a) for a, b in ((0, 1000), (1000, 1001), (1001, 3000))]
+        assert np.array_equal(np.concatenate([p[0] for p in parts]), whole)
+
+
+def _verify_fixed(frames: np.ndarray, proto: int):
+    """Vectorised RFC 1071 check of every frame (n, flen)."""
+    w = frames[:, 14:34].astype(np.uint32)
+    s = (w[:, 0::2] << 8 | w[:, 1::2]).sum(axis=1)
+    while (s >> 16).any():
+        s = (s & 0xFFFF) + (s >> 16)
+    assert (s == 0xFFFF).all(), "IPv4 checksum"
+    n, flen = frames.shape
+    seg = frames[:, 34:].astype(np.uint32)
+    if seg.shape[1] & 1:
+        seg = np.concatenate([seg, np.zeros((n, 1), np.uint32)], axis=1)
+    s = (seg[:, 0::2] << 8 | seg[:, 1::2]).sum(axis=1).astype(np.uint64)
+    ip = frames[:, 26:34].astype(np.uint64)
+    s += (ip[:, 0::2] << 8 | ip[:, 1::2]).sum(axis=1)
+    s += proto + (flen - 34)
+    while (s >> 16).any():
+        s = (s & 0xFFFF) + (s >> 16)
+    assert (s == 0xFFFF).all(), "L4 checksum"
+
+
+@pytest.mark.parametrize("name,n_iter", [("c2_udp_64", 1 << 25), ("c4_tcp_syn", 1 << 25), ("c2_udp_1500", 1 << 21)])
+def test_full_size_properties(ctx, name, n_iter):
+    """BASELINE.json sizes: every checksum of every frame verifies, and random
+    sampled frames equal the oracle's."""
+    cfg = pc.get(name)
+    seq = Sequence.from_config(cfg)
+    ctx.load_sequence(0, seq, pc.SEED_BASE)
+    mf, mb = ctx.build_size(0, n_iter)
+    fb = ctx.alloc_frames(mf, mb)
+    ctx.build(0, 0, n_iter, fb)
+    ctx.sync()
+    flen = int(fb.f.fixed_len)
+    assert flen > 0
+    data = fb.packed()
+    fb.free()
+    frames = data.reshape(n_iter, flen)
+    proto = 17 if cfg["ip"]["protocol"] == "udp" else 6
+    for lo in range(0, n_iter, 1 << 22):
+        _verify_fixed(frames[lo:lo + (1 << 22)], proto)
+    rng = np.random.default_rng(1)
+    for k in rng.integers(0, n_iter, 200):
+        want = ob.frames(seq, 0, int(k), 1, pc.SEED_BASE)[0]
+        assert frames[int(k)].tobytes() == want
+
+
+def test_variable_full_size_offsets(ctx):
+    """configs[2] at 2^22 frames: offsets are a prefix sum of lengths in
+    [106, 1542], every sampled frame equals the oracle's, every checksum verifies."""
+    cfg = pc.get("c3_udp_var")
+    seq = Sequence.from_config(cfg)
+    n = 1 << 22
+    ctx.load_sequence(0, seq, pc.SEED_BASE)
+    mf, mb = ctx.build_size(0, n)
+    fb = ctx.alloc_frames(mf, mb)
+    ctx.build(0, 0, n, fb)
+    ctx.sync()
+    off = fb.offsets()
+    data = fb.packed()
+    fb.free()
+    lens = np.diff(off.astype(np.int64))
+    assert lens.min() >= 106 and lens.max() <= 1542 and off[0] == 0
+    rng = np.random.default_rng(2)
+    for k in rng.integers(0, n, 300):
+        k = int(k)
+        got = data[int(off[k]):int(off[k + 1])].tobytes()
+        assert got == ob.frames(seq, 0, k, 1, pc.SEED_BASE)[0]
+        assert pv.ip_csum_ok(got) and pv.l4_csum_value(got) == pv.parse(got)["l4_csum"]
+
+
+def test_counters_and_umem_landing(ctx):
+    cfg = pc.get("c3_udp_var")
+    seq = Sequence.from_config(cfg)
+    ctx.load_sequence(7, seq, pc.SEED_BASE)
+    p0, b0 = ctx.counters(8)
+    mf, mb = ctx.build_size(7, 5000)
+    fb = ctx.alloc_frames(mf, mb)
+    ctx.build(7, 100, 5000, fb)
+    ctx.sync()
+    total = fb.total_bytes()
+    p1, b1 = ctx.counters(8)
+    assert int(p1[7] - p0[7]) == 5000 and int(b1[7] - b0[7]) == total
+    want = ob.frames(seq, 7, 100, 5000, pc.SEED_BASE)
+    umem = np.zeros(4096 * 1000, dtype=np.uint8)
+    lens = fb.to_umem(umem, 4096, 2000, 1000)
+    for j in range(1000):
+        assert lens[j] == len(want[2000 + j])
+        assert umem[j * 4096:j * 4096 + lens[j]].tobytes() == want[2000 + j]
+    fb.free()
+    # fixed length: 2-D copy into 4096-B slots
+    ctx.load_sequence(8, Sequence.from_config(pc.get("c2_udp_64")), pc.SEED_BASE)
+    fb = ctx.alloc_frames(*ctx.build_size(8, 4096))
+    ctx.build(8, 0, 4096, fb)
+    ctx.sync()
+    want = ob.frames(Sequence.from_config(pc.get("c2_udp_64")), 8, 0, 4096, pc.SEED_BASE)
+    umem = np.zeros(4096 * 4096, dtype=np.uint8)
+    lens = fb.to_umem(umem, 4096, 0, 4096)
+    assert (lens == 64).all()
+    for j in range(0, 4096, 97):
+        assert umem[j * 4096:j * 4096 + 64].tobytes() == want[j]
+    fb.free()
+
+
+def test_error_behaviour(ctx):
+    seq = Sequence.from_config(pc.get("c2_udp_64"))
+    ctx.load_sequence(0, seq, 1)
+    fb = ctx.alloc_frames(10, 640)
+    with pytest.raises(pbgpu.PbError) as e:
+        ctx.build(0, 0, 11, fb)
+    assert e.value.code == -28
+    with pytest.raises(pbgpu.PbError) as e:
+        ctx.build(200, 0, 1, fb)
+    assert e.value.code == -2
+    fb.free()
+    bad = pc.get("c2_udp_64")
+    bad["ip"]["ttl"] = {"min": 9, "max": 3}
+    with pytest.raises(pbgpu.PbError) as e:
+        ctx.load_sequence(1, Sequence.from_config(bad), 1)
+    assert e.value.code == -22
+    nodst = pc.get("c2_udp_64")
+    del nodst["ip"]["dip"]
+    with pytest.raises(pbgpu.PbError) as e:
+        ctx.load_sequence(1, Sequence.from_config(nodst), 1)
+    assert e.value.code == -22
+    with pytest.raises(pbgpu.PbError) as e:
+        ctx.load_sequence(1, Sequence.from_config(pc.get("udp_multi_payload")), 1, payload_rule=1)
+    assert e.value.code == -95
+
+
+def test_fill_probe_runs(ctx):
+    ms = ctx.fill_probe(1 << 30, 5)
+    gbps = (1 << 30) / (ms * 1e-3) / 1e9
+    assert 500 < gbps < 9000
