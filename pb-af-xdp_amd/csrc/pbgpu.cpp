@@ -657,7 +657,8 @@ int pbgpu_frames_alloc(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capaci
     capacity_bytes = (capacity_bytes + 15) & ~15ull;
     const uint64_t max_tiles = capacity_bytes / 4096 + 4; // tiles are >= 8 KiB (frames >= 42 B)
     const uint64_t nblocks = capacity_frames / PB_SCAN_FRAMES_PER_BLOCK + 1;
-    if (hipMalloc((void **)&f->data, capacity_bytes ? capacity_bytes : 16) != hipSuccess ||
+    // +64 B: word-granular readers (UMEM scatter) may touch a few bytes past the last frame
+    if (hipMalloc((void **)&f->data, capacity_bytes + 64) != hipSuccess ||
         hipMalloc((void **)&f->offsets, (capacity_frames + 1) * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc((void **)&f->tile_first, max_tiles * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&f->scan_tmp, nblocks * sizeof(uint64_t)) != hipSuccess)

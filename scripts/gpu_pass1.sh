@@ -1,0 +1,12 @@
+#!/bin/bash
+# first GPU pass: smoke, parity tests, short bench
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -30 gpurun_out/smoke.log; exit 1; }
+echo SMOKE_OK
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+tail -15 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 --cpu-seconds 4 > gpurun_out/bench1.log 2>&1; rc=$?
+tail -5 gpurun_out/bench1.log
+exit $rc

@@ -166,8 +166,9 @@ def test_counters_and_umem_landing(ctx):
     umem = np.zeros(4096 * 1000, dtype=np.uint8)
     lens = fb.to_umem(umem, 4096, 2000, 1000)
     for j in range(1000):
-        assert lens[j] == len(want[2000 + j])
-        assert umem[j * 4096:j * 4096 + lens[j]].tobytes() == want[2000 + j]
+        ln = int(lens[j])
+        assert ln == len(want[2000 + j])
+        assert umem[j * 4096:j * 4096 + ln].tobytes() == want[2000 + j]
     fb.free()
     # fixed length: 2-D copy into 4096-B slots
     ctx.load_sequence(8, Sequence.from_config(pc.get("c2_udp_64")), pc.SEED_BASE)
