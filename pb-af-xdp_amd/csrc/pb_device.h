@@ -90,6 +90,9 @@ struct pb_kargs
     uint32_t n_tiles;
     uint8_t *out;
     unsigned long long *counters; // [2] pckts, bytes of this sequence
+    uint32_t small_ndw;     // >0: small fixed frames, one lane per frame, NDW dwords per lane
+    uint32_t nt_stores;     // 1: non-temporal output stores
+    uint32_t stail[32];     // small kernel, static payload: payload bytes at frame dwords p0.. (p0 = (hl-2)/4)
 };
 
 __device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)

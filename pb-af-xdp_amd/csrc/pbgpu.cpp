@@ -605,6 +605,24 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     K.fixed_len = fixed ? minf : 0;
     if (fixed)
         K.flen = make_div(minf);
+    // small fixed frames: one lane per frame (pb_small_kernel)
+    if (fixed && pls.size() == 1 && minf <= 128)
+    {
+        K.small_ndw = minf <= 64 ? 16 : 32;
+        if (!pls[0].random)
+        {
+            const uint32_t p0 = (K.hl - 2) / 4;
+            for (uint32_t j = 0; j < pls[0].slen; ++j)
+            {
+                const uint32_t pos = K.hl + j;
+                K.stail[pos / 4 - p0] |= (uint32_t)blob[pls[0].blob_off + j] << (8 * (pos % 4));
+            }
+        }
+    }
+    {
+        const char *nt = getenv("PBGPU_NT");
+        K.nt_stores = (nt && atoi(nt)) ? 1 : 0;
+    }
     // tile: power of two, <= 16 KiB, <= (PB_NF_MAX - 2) frames of minimum length
     uint32_t cap = (PB_NF_MAX - 2) * minf;
     uint32_t shift = 14;

@@ -156,7 +156,51 @@ __device__ __forceinline__ uint32_t pb_window(const uint32_t *img, int x)
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
+// Header image of one frame (sequence.c:150-258 template + sequence.c:443-527
+// per-iteration fields + tot_len / udp len + IPv4 checksum, sequence.c:596-602),
+// frame bytes 0..63 as little-endian dwords; the L4 checksum field stays 0.
+// Returns the L4 length (header + payload).
+__device__ __forceinline__ uint32_t pb_header(const pb_kargs &K, uint32_t r0, uint32_t plen, uint32_t (&d)[16])
+{
+    const uint32_t flags = K.flags;
+#pragma unroll
+    for (int w = 0; w < 16; ++w)
+        d[w] = K.tmpl[w];
+    if (flags & PBK_RND_TTL) // sequence.c:443-446
+        d[5] |= ((K.ttl_min + pb_mod(r0, K.ttl)) & 0xFFu) << 16;
+    if (flags & PBK_RND_ID) // sequence.c:449-452
+        d[4] |= pb_bswap16((K.id_min + pb_mod(r0, K.id)) & 0xFFFFu) << 16;
+    if (flags & PBK_RND_SADDR) // sequence.c:455-497
+    {
+        const uint2 rg = K.ranges[K.rng.d == 1 ? 0u : pb_mod(r0, K.rng)];
+        const uint32_t sa = __builtin_bswap32(rg.x | (r0 & rg.y));
+        d[6] |= sa << 16;
+        d[7] |= sa >> 16;
+    }
+    if (flags & (PBK_RND_SPORT | PBK_RND_DPORT)) // sequence.c:500-527
+    {
+        const uint32_t port = pb_bswap16(1u + pb_mod(r0, K.port));
+        if (flags & PBK_RND_SPORT)
+            d[8] |= port << 16;
+        if (flags & PBK_RND_DPORT)
+            d[9] |= port;
+    }
+    const uint32_t l4tot = K.l4len + plen;
+    d[4] |= pb_bswap16(20u + l4tot); // tot_len, sequence.c:597
+    if (K.proto == 17u)
+        d[9] |= pb_bswap16(l4tot) << 16; // udph->len, sequence.c:567
+    if (flags & PBK_IP_CSUM) // update_iph_checksum, sequence.c:599-602
+    {
+        const uint32_t sum = (d[3] >> 16) + pb_halves(d[4]) + pb_halves(d[5]) + (d[6] >> 16) + pb_halves(d[7]) +
+                             (d[8] & 0xFFFFu);
+        const uint32_t c = (flags & PBK_IPH_SINGLE) ? ~((sum & 0xFFFFu) + (sum >> 16)) : ~pb_fold(sum);
+        d[6] |= c & 0xFFFFu;
+    }
+    return l4tot;
+}
+
 } // namespace
+
 
 // One payload byte = three glibc LCG steps: x -> A3 * x + C3 (mod 2^32).
 constexpr uint32_t PB_A3 = PB_LCG_A * PB_LCG_A * PB_LCG_A;
@@ -235,41 +279,7 @@ __global__ __launch_bounds__(PB_WG) void pb_build_kernel(pb_kargs K)
         const pb_frame_pl P = pb_payload(K, s, pi);
 
         uint32_t d[16];
-#pragma unroll
-        for (int w = 0; w < 16; ++w)
-            d[w] = K.tmpl[w];
-
-        if (flags & PBK_RND_TTL) // sequence.c:443-446
-            d[5] |= ((K.ttl_min + pb_mod(r0, K.ttl)) & 0xFFu) << 16;
-        if (flags & PBK_RND_ID) // sequence.c:449-452
-            d[4] |= pb_bswap16((K.id_min + pb_mod(r0, K.id)) & 0xFFFFu) << 16;
-        if (flags & PBK_RND_SADDR) // sequence.c:455-497
-        {
-            const uint2 rg = K.ranges[pb_mod(r0, K.rng)];
-            const uint32_t sa = __builtin_bswap32(rg.x | (r0 & rg.y));
-            d[6] |= sa << 16;
-            d[7] |= sa >> 16;
-        }
-        if (flags & (PBK_RND_SPORT | PBK_RND_DPORT)) // sequence.c:500-527
-        {
-            const uint32_t port = pb_bswap16(1u + pb_mod(r0, K.port));
-            if (flags & PBK_RND_SPORT)
-                d[8] |= port << 16;
-            if (flags & PBK_RND_DPORT)
-                d[9] |= port;
-        }
-        const uint32_t l4tot = K.l4len + P.plen;
-        d[4] |= pb_bswap16(20u + l4tot); // tot_len, sequence.c:597
-        if (K.proto == 17u)
-            d[9] |= pb_bswap16(l4tot) << 16; // udph->len, sequence.c:567
-
-        if (flags & PBK_IP_CSUM) // update_iph_checksum, sequence.c:599-602
-        {
-            const uint32_t sum = (d[3] >> 16) + pb_halves(d[4]) + pb_halves(d[5]) + (d[6] >> 16) +
-                                 pb_halves(d[7]) + (d[8] & 0xFFFFu);
-            const uint32_t c = (flags & PBK_IPH_SINGLE) ? ~((sum & 0xFFFFu) + (sum >> 16)) : ~pb_fold(sum);
-            d[6] |= c & 0xFFFFu;
-        }
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d);
 
         // L4 header words (check field still 0) + pseudo header
         uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) +
@@ -467,6 +477,168 @@ __global__ __launch_bounds__(PB_WG) void pb_build_kernel(pb_kargs K)
     }
 }
 
+// ---------------- small fixed-length frames: one lane per frame ----------------
+//
+// Frames of <= 4*NDW bytes (configs[1] 64-B UDP, configs[3] 60-B TCP SYN, the
+// 98/106-B ICMP/UDP frames): each lane builds its whole frame in NDW VGPRs
+// (header, payload, both checksums — sequence.c:433-602 for one iteration),
+// writes it into an LDS tile at its packed byte offset, and the workgroup then
+// streams the tile (256 frames, always a multiple of 16 B) to HBM with
+// contiguous 16-B stores.  PROTO (17/6/1) fixes the header length and the
+// checksum position at compile time; RANDOM selects the payload source.  The
+// frame body is straight-line code (no data-dependent control flow on d[]).
+
+// keep bytes [lo, hi) of a dword (byte positions 0..3), branch-free
+__device__ __forceinline__ uint32_t pb_range_mask(int lo, int hi)
+{
+    lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+    hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
+    const uint32_t ge = (uint32_t)(0xFFFFFFFFull << (8 * lo));
+    const uint32_t lt = (uint32_t)((1ull << (8 * hi)) - 1ull);
+    return ge & lt;
+}
+
+template <int NDW, int PROTO, bool RANDOM>
+__global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
+{
+    constexpr int HL = PROTO == 6 ? 54 : 42;
+    constexpr int P0 = (HL - 2) / 4;                                 // payload byte 0 = byte 2 of dword P0
+    constexpr int CDW = PROTO == 17 ? 10 : (PROTO == 6 ? 12 : 9);   // L4 checksum dword
+    constexpr int CSH = PROTO == 6 ? 16 : 0;                         // ... and its half
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[PB_WG * NDW + 8];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t f0 = (uint64_t)blockIdx.x * PB_WG;
+    const uint64_t left = K.n_frames - f0;
+    const uint32_t nfr = left < PB_WG ? (uint32_t)left : PB_WG;
+    const uint32_t flen = K.fixed_len;
+    const uint32_t flags = K.flags;
+
+    if (tid < nfr)
+    {
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + f0 + tid);
+        const uint32_t r0 = pb_rand_r(s);
+        const uint32_t plen = flen - HL;
+        uint32_t h[16];
+        const uint32_t l4tot = pb_header(K, r0, plen, h);
+        uint32_t d[NDW];
+#pragma unroll
+        for (int t = 0; t < NDW; ++t)
+            d[t] = t < 16 ? h[t] : 0u;
+
+        if (RANDOM)
+        {
+            // single payload: its draws start from the iteration seed (sequence.c:548-555)
+            const uint32_t a3 = PB_A3, c3 = PB_C3;
+            const int nv = (int)((flags & PBK_LITERAL) ? min(plen, 1u) : plen);
+            uint32_t y0 = pb_step3(s, a3, c3), y1 = pb_step3(y0, a3, c3);
+            uint32_t x = y1;
+            d[P0] |= __builtin_amdgcn_perm(y1, y0, 0x06020C0Cu) & pb_range_mask(HL - 4 * P0, HL + nv - 4 * P0);
+#pragma unroll
+            for (int t = P0 + 1; t < NDW; ++t)
+            {
+                const uint32_t x0 = pb_step3(x, a3, c3), x1 = pb_step3(x0, a3, c3);
+                const uint32_t x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+                x = x3;
+                d[t] |= pb_pack4(x0, x1, x2, x3) & pb_range_mask(0, HL + nv - 4 * t);
+            }
+        }
+        else
+        {
+#pragma unroll
+            for (int t = P0; t < NDW; ++t)
+                d[t] |= K.stail[t - P0];
+        }
+        // bytes past the frame end
+#pragma unroll
+        for (int t = 0; t < NDW; ++t)
+            d[t] &= pb_range_mask(0, (int)flen - 4 * t);
+
+        // L4 checksum (csum_tcpudp_magic / icmp_csum, sequence.c:569-594)
+        uint32_t sum = d[8] >> 16;
+#pragma unroll
+        for (int t = 9; t < NDW; ++t)
+            sum += pb_halves(d[t]);
+        if (PROTO != 1)
+            sum += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((PROTO + l4tot) << 8);
+        const uint32_t c = (flags & PBK_L4_CSUM) ? ((~pb_fold(sum)) & 0xFFFFu) : 0u;
+        d[CDW] |= c << CSH;
+
+        // frame -> LDS tile at byte offset tid * flen
+        const uint32_t B = tid * flen;
+        if ((flen & 15u) == 0)
+        {
+#pragma unroll
+            for (int t = 0; t < NDW; t += 4)
+                if ((uint32_t)(4 * t) < flen)
+                    *reinterpret_cast<pb_u32x4 *>(s_tile + (B >> 2) + t) = pb_u32x4{d[t], d[t + 1], d[t + 2], d[t + 3]};
+        }
+        else if ((flen & 7u) == 0)
+        {
+#pragma unroll
+            for (int t = 0; t < NDW; t += 2)
+                if ((uint32_t)(4 * t) < flen)
+                    *reinterpret_cast<uint2 *>(s_tile + (B >> 2) + t) = make_uint2(d[t], d[t + 1]);
+        }
+        else if ((flen & 3u) == 0)
+        {
+#pragma unroll
+            for (int t = 0; t < NDW; ++t)
+                if ((uint32_t)(4 * t) < flen)
+                    s_tile[(B >> 2) + t] = d[t];
+        }
+        else
+        {
+            // frame starts at byte phase sh of a dword: out dword u = frame bytes [4u - sh, 4u - sh + 4)
+            const uint32_t sh = B & 3u;
+            uint32_t *row = s_tile + (B >> 2);
+            uint8_t *rowb = reinterpret_cast<uint8_t *>(row);
+            const uint32_t end = sh + flen; // row bytes this frame owns: [sh, end)
+#pragma unroll
+            for (int u = 0; u <= NDW; ++u)
+            {
+                if ((uint32_t)(4 * u) < end)
+                {
+                    const uint32_t lo = u > 0 ? d[u - 1] : 0u;
+                    const uint32_t hi = u < NDW ? d[u] : 0u;
+                    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
+                    const uint32_t b0 = u == 0 ? sh : 0u;
+                    const uint32_t b1 = end - 4 * u < 4 ? end - 4 * u : 4u;
+                    if (b0 == 0 && b1 == 4)
+                        row[u] = v;
+                    else
+                        for (uint32_t b = b0; b < b1; ++b)
+                            rowb[4 * u + b] = (uint8_t)(v >> (8 * b));
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // tile -> HBM: contiguous 16-B stores (every full tile is a multiple of 16 B)
+    const uint32_t tile_bytes = nfr * flen;
+    const uint32_t nchunks = (tile_bytes + 15) >> 4;
+    uint8_t *const out = K.out + f0 * flen;
+    for (uint32_t c = tid; c < nchunks; c += PB_WG)
+    {
+        pb_u32x4 v = *reinterpret_cast<const pb_u32x4 *>(s_tile + 4 * c);
+        if (16 * c + 16 > tile_bytes) // last chunk of the stream: zero the tail
+        {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                v[t] &= pb_range_mask(0, (int)tile_bytes - (int)(16 * c + 4 * t));
+        }
+        if (K.nt_stores)
+            __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(out + 16 * c));
+        else
+            *reinterpret_cast<pb_u32x4 *>(out + 16 * c) = v;
+    }
+    if (blockIdx.x == 0 && tid == 0)
+    {
+        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
+        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+    }
+}
+
 // ---------------- variable length: lengths -> offsets -> tile map ----------------
 
 __global__ __launch_bounds__(256) void pb_len_reduce(pb_kargs K, unsigned long long *block_sums)
@@ -598,9 +770,37 @@ __global__ __launch_bounds__(256) void pb_fill_kernel(pb_u32x4 *dst, uint64_t n1
 
 // ---------------- launch wrappers (called from pbgpu.cpp) ----------------
 
+template <int NDW, int PROTO>
+static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
+{
+    if (K->pl0.random)
+        hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true>), dim3(grid), dim3(PB_WG), 0, st, *K);
+    else
+        hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false>), dim3(grid), dim3(PB_WG), 0, st, *K);
+}
+
+template <int NDW>
+static void pbk_launch_small(const pb_kargs *K, uint32_t grid, hipStream_t st)
+{
+    if (K->proto == 17)
+        pbk_launch_small_p<NDW, 17>(K, grid, st);
+    else if (K->proto == 6)
+        pbk_launch_small_p<NDW, 6>(K, grid, st);
+    else
+        pbk_launch_small_p<NDW, 1>(K, grid, st);
+}
+
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid, hipStream_t st)
 {
-    if (K->fixed_len)
+    if (K->small_ndw)
+    {
+        const uint32_t grid = (uint32_t)((K->n_frames + PB_WG - 1) / PB_WG);
+        if (K->small_ndw == 16)
+            pbk_launch_small<16>(K, grid, st);
+        else
+            pbk_launch_small<32>(K, grid, st);
+    }
+    else if (K->fixed_len)
         hipLaunchKernelGGL(pb_build_kernel<true>, dim3(n_tiles_grid), dim3(PB_WG), 0, st, *K);
     else
         hipLaunchKernelGGL(pb_build_kernel<false>, dim3(n_tiles_grid), dim3(PB_WG), 0, st, *K);
