@@ -563,28 +563,42 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
         const uint32_t c = (flags & PBK_L4_CSUM) ? ((~pb_fold(sum)) & 0xFFFFu) : 0u;
         d[CDW] |= c << CSH;
 
-        // frame -> LDS tile at byte offset tid * flen
+        // frame -> LDS tile at byte offset tid * flen.  16/8-B aligned frames go
+        // through an XOR swizzle of the 16-B slots (slot ^ (slot >> 3) & 7) so
+        // lanes at a 64-B stride hit distinct banks; the copy-out undoes it.
         const uint32_t B = tid * flen;
         if ((flen & 15u) == 0)
         {
+            pb_u32x4 *tile16 = reinterpret_cast<pb_u32x4 *>(s_tile);
+            const uint32_t slot0 = tid * (flen >> 4);
 #pragma unroll
             for (int t = 0; t < NDW; t += 4)
                 if ((uint32_t)(4 * t) < flen)
-                    *reinterpret_cast<pb_u32x4 *>(s_tile + (B >> 2) + t) = pb_u32x4{d[t], d[t + 1], d[t + 2], d[t + 3]};
+                {
+                    const uint32_t sl = slot0 + (t >> 2);
+                    tile16[sl ^ ((sl >> 3) & 7u)] = pb_u32x4{d[t], d[t + 1], d[t + 2], d[t + 3]};
+                }
         }
         else if ((flen & 7u) == 0)
         {
+            uint2 *tile8 = reinterpret_cast<uint2 *>(s_tile);
+            const uint32_t q0 = tid * (flen >> 3);
 #pragma unroll
             for (int t = 0; t < NDW; t += 2)
                 if ((uint32_t)(4 * t) < flen)
-                    *reinterpret_cast<uint2 *>(s_tile + (B >> 2) + t) = make_uint2(d[t], d[t + 1]);
+                {
+                    const uint32_t q = q0 + (t >> 1);
+                    const uint32_t sl = q >> 1;
+                    tile8[((sl ^ ((sl >> 3) & 7u)) << 1) | (q & 1u)] = make_uint2(d[t], d[t + 1]);
+                }
         }
         else if ((flen & 3u) == 0)
         {
+            const uint32_t w0 = tid * (flen >> 2);
 #pragma unroll
             for (int t = 0; t < NDW; ++t)
                 if ((uint32_t)(4 * t) < flen)
-                    s_tile[(B >> 2) + t] = d[t];
+                    s_tile[w0 + t] = d[t];
         }
         else
         {
@@ -618,9 +632,11 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
     const uint32_t tile_bytes = nfr * flen;
     const uint32_t nchunks = (tile_bytes + 15) >> 4;
     uint8_t *const out = K.out + f0 * flen;
+    const bool swz = (flen & 7u) == 0;
     for (uint32_t c = tid; c < nchunks; c += PB_WG)
     {
-        pb_u32x4 v = *reinterpret_cast<const pb_u32x4 *>(s_tile + 4 * c);
+        const uint32_t sl = swz ? (c ^ ((c >> 3) & 7u)) : c;
+        pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[sl];
         if (16 * c + 16 > tile_bytes) // last chunk of the stream: zero the tail
         {
 #pragma unroll
