@@ -17,7 +17,7 @@
 #define PB_TILE_MAX (PB_WG * PB_CPL * 16)  // 16 KiB of output per workgroup
 #define PB_NF_MAX 260                      // frames touching one tile, max
 #define PB_IMG_DW 16                       // header image: 64 B per frame
-#define PB_JNEG 16                         // jump table starts at j = -16
+#define PB_JNEG 80                         // jump table starts at j = -80
 
 // glibc LCG
 #define PB_LCG_A 1103515245u
@@ -91,6 +91,8 @@ struct pb_kargs
     uint8_t *out;
     unsigned long long *counters; // [2] pckts, bytes of this sequence
     uint32_t small_ndw;     // >0: small fixed frames, one lane per frame, NDW dwords per lane
+    uint32_t gpf_g;         // >0: group-per-frame kernel with G lanes per frame
+    const uint2 *lcg48;     // lcg48[m] = L^(48 m): one 16-B chunk of payload = 48 LCG steps
     uint32_t nt_stores;     // 1: non-temporal output stores
     uint32_t stail[32];     // small kernel, static payload: payload bytes at frame dwords p0.. (p0 = (hl-2)/4)
 };

@@ -28,7 +28,7 @@ extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *off
                                          uint8_t *dst, uint32_t stride, uint16_t *lens, hipStream_t st);
 extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, hipStream_t st);
 
-#define PB_JUMP_N (65536 + 64) // entries j = -16 .. 65583
+#define PB_JUMP_N (65536 + 256) // entries j = -PB_JNEG .. 65536 + 175
 #define PB_SCAN_FRAMES_PER_BLOCK (256 * 8)
 
 namespace
@@ -79,6 +79,7 @@ struct pbgpu_ctx
     int device = 0;
     hipStream_t stream = nullptr;
     uint2 *d_jump = nullptr;
+    uint2 *d_lcg48 = nullptr;
     unsigned long long *d_counters = nullptr; // [PB_MAX_SEQUENCES][4]
     seq_slot seqs[PB_MAX_SEQUENCES];
     std::vector<timing_pair> pending;
@@ -132,7 +133,7 @@ std::vector<uint2> make_jump_table()
         ainv *= 2u - a * ainv;
     // inverse step y -> ainv * (y - c)
     const uint32_t ia = ainv, ic = (uint32_t)(0u - ainv * c);
-    // E(-16) = L^(-45)
+    // first entry: j = -PB_JNEG -> L^(3(1 - PB_JNEG))
     uint32_t A = 1, C = 0;
     for (int i = 0; i < 3 * (PB_JNEG - 1); ++i)
     {
@@ -318,7 +319,21 @@ int pbgpu_open(int device, pbgpu_ctx **out)
         return PBGPU_EIO;
     }
     std::vector<uint2> jt = make_jump_table();
-    if (upload(&ctx->d_jump, jt.data(), jt.size()) != PBGPU_OK ||
+    std::vector<uint2> l48(65);
+    {
+        const uint32_t a3 = PB_LCG_A * PB_LCG_A * PB_LCG_A, c3 = PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u);
+        uint32_t A16 = 1, C16 = 0; // L^48 = (L^3)^16
+        for (int i = 0; i < 16; ++i)
+            C16 = a3 * C16 + c3, A16 = a3 * A16;
+        uint32_t A = 1, C = 0;
+        for (int m = 0; m < 65; ++m)
+        {
+            l48[m] = make_uint2(A, C);
+            A = A16 * A;
+            C = A16 * C + C16;
+        }
+    }
+    if (upload(&ctx->d_jump, jt.data(), jt.size()) != PBGPU_OK || upload(&ctx->d_lcg48, l48.data(), l48.size()) != PBGPU_OK ||
         hipMalloc((void **)&ctx->d_counters, sizeof(unsigned long long) * 4 * PB_MAX_SEQUENCES) != hipSuccess ||
         hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * 4 * PB_MAX_SEQUENCES) != hipSuccess)
     {
@@ -347,6 +362,8 @@ void pbgpu_close(pbgpu_ctx *ctx)
     }
     if (ctx->d_jump)
         (void)hipFree(ctx->d_jump);
+    if (ctx->d_lcg48)
+        (void)hipFree(ctx->d_lcg48);
     if (ctx->d_counters)
         (void)hipFree(ctx->d_counters);
     if (ctx->h_stage)
@@ -501,7 +518,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
 
     // payloads, sequence.c:264-374
     std::vector<pb_pl> pls;
-    std::vector<uint8_t> blob(16, 0);
+    std::vector<uint8_t> blob(96, 0); // >= 80 B of zeros before every static payload
     uint16_t dl_setup[PB_MAX_PAYLOADS];
     memset(dl_setup, 0, sizeof dl_setup);
     uint32_t sseed = host_seed(seed_base, seq_idx, PB_STATIC_SEED_K); // quirk B2
@@ -548,7 +565,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             P.blob_off = (uint32_t)blob.size();
             P.ssum = le_word_sum(bytes.data(), bytes.size());
             blob.insert(blob.end(), bytes.begin(), bytes.end());
-            blob.insert(blob.end(), 48 - (bytes.size() & 15), 0); // >= 32 B zero pad, 16-B aligned
+            blob.insert(blob.end(), 96 + 16 - (bytes.size() & 15), 0); // >= 96 B zero pad, 16-B aligned
         }
         else if (po->max_len > 0)
         {
@@ -565,7 +582,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         {
             P.random = 0; // non-static, max_len 0: empty payload (sequence.c:557-560)
             P.slen = 0;
-            P.blob_off = 16;
+            P.blob_off = 16 + 64;
         }
         if (K.hl + (P.random ? po->max_len : P.slen) > PB_MAX_PCKT_LEN)
             return PBGPU_EINVAL;
@@ -575,7 +592,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     {
         pb_pl P;
         memset(&P, 0, sizeof P);
-        P.blob_off = 16;
+        P.blob_off = 16 + 64;
         pls.push_back(P);
     }
     if ((flags & PBK_LITERAL) && pls.size() > 1 && n_random > 0)
@@ -622,6 +639,12 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     {
         const char *nt = getenv("PBGPU_NT");
         K.nt_stores = (nt && atoi(nt)) ? 1 : 0;
+        const char *kern = getenv("PBGPU_KERNEL"); // "tile": force the tile kernel (comparison only)
+        const bool tile = kern && !strcmp(kern, "tile");
+        if (tile)
+            K.small_ndw = 0;
+        else if (!K.small_ndw)
+            K.gpf_g = maxf <= 320 ? 8 : 32;
     }
     // tile: power of two, <= 16 KiB, <= (PB_NF_MAX - 2) frames of minimum length
     uint32_t cap = (PB_NF_MAX - 2) * minf;
@@ -643,6 +666,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     K.pls = S.d_pls;
     K.blob = S.d_blob;
     K.jump = ctx->d_jump;
+    K.lcg48 = ctx->d_lcg48;
     K.counters = ctx->d_counters + 4 * seq_idx;
     S.K = K;
     S.loaded = true;

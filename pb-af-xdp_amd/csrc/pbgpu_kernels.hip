@@ -655,6 +655,219 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
     }
 }
 
+// ---------------- group per frame: any length, fixed or packed variable ----------------
+//
+// Workgroup = 256 frames.  Phase A: one lane per frame computes the seed,
+// fields, header image + IPv4 checksum (sequence.c:433-527, 596-602) into LDS.
+// Phase B: a group of G lanes streams one frame at a time: lane l of the group
+// produces the frame's output-aligned 16-B chunks l, l+G, ... (payload bytes
+// from the glibc LCG, sequence.c:552-555, jumped to the chunk start with
+// per-lane constants L^(48 l) and advanced by L^(48 G) per step), stores every
+// chunk that holds no header byte straight away, sums the payload words for
+// the L4 checksum (sequence.c:569-594), reduces that sum across the group with
+// lane shuffles, and finally stores the header chunks with the finished
+// checksum.  Chunks shared with a neighbouring frame are written byte/dword-
+// masked, so every byte of the packed stream is written exactly once.
+
+// store bytes [max(0,-q0), min(16, flen-q0)) of a 16-B chunk at p (16-B aligned)
+__device__ __forceinline__ void pb_store_chunk(uint8_t *p, uint32_t o0, uint32_t o1, uint32_t o2, uint32_t o3, int q0,
+                                               int flen, uint32_t nt)
+{
+    const int a = -q0, b = flen - q0;
+    if (a <= 0 && b >= 16)
+    {
+        if (nt)
+            __builtin_nontemporal_store(pb_u32x4{o0, o1, o2, o3}, reinterpret_cast<pb_u32x4 *>(p));
+        else
+            *reinterpret_cast<pb_u32x4 *>(p) = pb_u32x4{o0, o1, o2, o3};
+        return;
+    }
+    const uint32_t o[4] = {o0, o1, o2, o3};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+    {
+        const int lo = max(a - 4 * t, 0), hi = min(b - 4 * t, 4);
+        if (lo == 0 && hi == 4)
+            *reinterpret_cast<uint32_t *>(p + 4 * t) = o[t];
+        else
+            for (int i = lo; i < hi; ++i)
+                p[4 * t + i] = (uint8_t)(o[t] >> (8 * i));
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_img[PB_WG * PB_IMG_STRIDE];
+    __shared__ uint32_t s_blo[PB_WG], s_bhi[PB_WG], s_flen[PB_WG], s_z[PB_WG], s_nv[PB_WG], s_src[PB_WG],
+        s_hsum[PB_WG];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t flags = K.flags;
+    const uint64_t fwg = (uint64_t)blockIdx.x * PB_WG;
+    const uint64_t left = K.n_frames - fwg;
+    const uint32_t nfr = left < PB_WG ? (uint32_t)left : PB_WG;
+    const int hl = (int)K.hl;
+
+    // ---------------- phase A: one lane per frame ----------------
+    if (tid < nfr)
+    {
+        const uint64_t f = fwg + tid;
+        uint64_t base;
+        uint32_t flen;
+        if (K.fixed_len)
+        {
+            base = f * K.fixed_len;
+            flen = K.fixed_len;
+        }
+        else
+        {
+            base = K.offsets[f];
+            flen = (uint32_t)(K.offsets[f + 1] - base);
+        }
+        uint64_t k;
+        uint32_t pi;
+        pb_frame_index(K, f, k, pi);
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+        const uint32_t r0 = pb_rand_r(s);
+        const pb_frame_pl P = pb_payload(K, s, pi);
+        uint32_t d[16];
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d);
+        uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) + pb_halves(d[12]) +
+                      pb_halves(d[13]);
+        if (flags & PBK_PSEUDO)
+            hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
+        if (!P.random)
+            hs += P.ssum;
+        pb_u32x4 *row = reinterpret_cast<pb_u32x4 *>(s_img + tid * PB_IMG_STRIDE);
+        row[0] = pb_u32x4{d[0], d[1], d[2], d[3]};
+        row[1] = pb_u32x4{d[4], d[5], d[6], d[7]};
+        row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
+        row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
+        row[4] = pb_u32x4{0u, 0u, 0u, 0u};
+        // LCG state for the payload byte at the first chunk's first position:
+        // j = -(base % 16 + hl), i.e. L^(3(1 - base % 16 - hl))(st0)
+        const uint2 jt = K.jump[PB_JNEG - ((uint32_t)(base & 15u) + (uint32_t)hl)];
+        s_blo[tid] = (uint32_t)base;
+        s_bhi[tid] = (uint32_t)(base >> 32);
+        s_flen[tid] = flen;
+        s_z[tid] = P.random ? jt.x * P.st0 + jt.y : 0u;
+        s_nv[tid] = P.nvalid | (P.random << 31);
+        s_src[tid] = P.blob_off;
+        s_hsum[tid] = hs;
+    }
+    __syncthreads();
+
+    // ---------------- phase B: G lanes per frame ----------------
+    constexpr uint32_t NG = 64 / G; // frames in flight per wave
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
+    const uint32_t g = lane / G, lg = lane % G;
+    const uint2 Ml = K.lcg48[lg], MG = K.lcg48[G];
+    const uint32_t a3 = PB_A3, c3 = PB_C3;
+    const uint32_t nt = K.nt_stores;
+
+    for (uint32_t p = 0; p < 64 / NG; ++p)
+    {
+        const uint32_t fr = wave * 64 + p * NG + g;
+        if (fr >= nfr)
+            continue;
+        const uint64_t base = ((uint64_t)s_bhi[fr] << 32) | s_blo[fr];
+        const int flen = (int)s_flen[fr];
+        const int s0 = (int)(base & 15u);
+        const uint32_t nch = (uint32_t)(s0 + flen + 15) >> 4;
+        const uint32_t nv = s_nv[fr];
+        const bool rnd = (nv >> 31) != 0;
+        const int nvalid = (int)(nv & 0x7FFFFFFFu);
+        const uint32_t src = s_src[fr];
+        uint8_t *const out = K.out + (base & ~15ull);
+        uint32_t x = __umul24(s_z[fr], Ml.x) + Ml.y;
+        uint32_t acc = 0;
+        uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+        int hq = 0;
+        bool held = false;
+
+        for (uint32_t m = lg; m < nch; m += G)
+        {
+            const int q0 = (int)(16 * m) - s0; // frame position of the chunk's first byte
+            const int j0 = q0 - hl;            // payload index of the chunk's first byte
+            uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+            if (j0 < nvalid && j0 + 16 > 0)
+            {
+                if (rnd)
+                {
+                    uint32_t x0 = x, x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+                    o0 = pb_pack4(x0, x1, x2, x3);
+                    x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+                    o1 = pb_pack4(x0, x1, x2, x3);
+                    x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+                    o2 = pb_pack4(x0, x1, x2, x3);
+                    x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+                    o3 = pb_pack4(x0, x1, x2, x3);
+                }
+                else
+                {
+                    const uint8_t *bp = K.blob + src + j0;
+                    const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)bp & ~(uintptr_t)3);
+                    const uint32_t sh = (uint32_t)((uintptr_t)bp & 3);
+                    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+                    o0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                    o1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                    o2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+                    o3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
+                }
+                const int lo = -j0, hi = nvalid - j0; // valid payload bytes of the chunk: [lo, hi)
+                if (lo > 0 || hi < 16)
+                {
+                    o0 &= pb_range_mask(lo, hi);
+                    o1 &= pb_range_mask(lo - 4, hi - 4);
+                    o2 &= pb_range_mask(lo - 8, hi - 8);
+                    o3 &= pb_range_mask(lo - 12, hi - 12);
+                }
+                if (rnd)
+                    acc += pb_halves(o0) + pb_halves(o1) + pb_halves(o2) + pb_halves(o3);
+            }
+            if (q0 < hl)
+            {
+                h0 = o0, h1 = o1, h2 = o2, h3 = o3;
+                hq = q0;
+                held = true;
+            }
+            else
+            {
+                pb_store_chunk(out + 16 * m, o0, o1, o2, o3, q0, flen, nt);
+            }
+            x = __umul24(x, MG.x) + MG.y;
+        }
+#pragma unroll
+        for (int w = 1; w < G; w <<= 1)
+            acc += __shfl_xor(acc, w, 64);
+        if ((flags & PBK_L4_CSUM) && lg == 0)
+        {
+            uint32_t pc = pb_fold(acc);
+            if (base & 1u) // chunk sums were taken in output alignment
+                pc = pb_bswap16(pc);
+            const uint32_t c = (~pb_fold(pb_fold(s_hsum[fr]) + pc)) & 0xFFFFu;
+            s_img[fr * PB_IMG_STRIDE + K.csum_dw] |= K.csum_hi ? (c << 16) : c;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (held)
+        {
+            const uint32_t *img = s_img + fr * PB_IMG_STRIDE;
+            h0 |= pb_window(img, hq);
+            h1 |= pb_window(img, hq + 4);
+            h2 |= pb_window(img, hq + 8);
+            h3 |= pb_window(img, hq + 12);
+            pb_store_chunk(out + (hq + s0), h0, h1, h2, h3, hq, flen, nt);
+        }
+    }
+    if (K.fixed_len && blockIdx.x == 0 && tid == 0)
+    {
+        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
+        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+    }
+}
+
 // ---------------- variable length: lengths -> offsets -> tile map ----------------
 
 __global__ __launch_bounds__(256) void pb_len_reduce(pb_kargs K, unsigned long long *block_sums)
@@ -808,7 +1021,15 @@ static void pbk_launch_small(const pb_kargs *K, uint32_t grid, hipStream_t st)
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid, hipStream_t st)
 {
-    if (K->small_ndw)
+    if (K->gpf_g)
+    {
+        const uint32_t grid = (uint32_t)((K->n_frames + PB_WG - 1) / PB_WG);
+        if (K->gpf_g == 8)
+            hipLaunchKernelGGL((pb_gpf_kernel<8>), dim3(grid), dim3(PB_WG), 0, st, *K);
+        else
+            hipLaunchKernelGGL((pb_gpf_kernel<32>), dim3(grid), dim3(PB_WG), 0, st, *K);
+    }
+    else if (K->small_ndw)
     {
         const uint32_t grid = (uint32_t)((K->n_frames + PB_WG - 1) / PB_WG);
         if (K->small_ndw == 16)
