@@ -82,6 +82,7 @@ def run_config(ctx, name, seq_idx, n_pkts, steps, warmup, rank, world, dist, loc
         ctx.build(seq_idx, step_iter(s), n_pkts, fb)
     ctx.sync()
     ctx.kernel_time()  # drop warm-up launches
+    p0, b0 = ctx.counters(seq_idx + 1)
     barrier(dist, local)
     t0 = time.perf_counter()
     for s in range(steps):
@@ -99,6 +100,9 @@ def run_config(ctx, name, seq_idx, n_pkts, steps, warmup, rank, world, dist, loc
     wall = time.perf_counter() - t0
     k_ms, k_n = ctx.kernel_time()
     flen = int(fb.f.fixed_len)
+    p1, b1 = ctx.counters(seq_idx + 1)
+    bytes_per_launch = int(b1[seq_idx] - b0[seq_idx]) // steps  # this rank's frame bytes per launch
+    kernel = ctx.kernel_name(seq_idx)
     fb.free()
     if dist is not None:
         import torch
@@ -107,7 +111,7 @@ def run_config(ctx, name, seq_idx, n_pkts, steps, warmup, rank, world, dist, loc
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
     return {"wall_s": wall, "kernel_ms_avg": k_ms / max(k_n, 1), "kernel_launches": k_n, "flen": flen,
-            "counters": counters}
+            "counters": counters, "bytes_per_launch": bytes_per_launch, "kernel": kernel}
 
 
 def d2h_rate(ctx, seq_idx, n_pkts):
@@ -168,24 +172,31 @@ def main():
     ctx = GpuContext(local)
     res = run_config(ctx, a.config, 0, a.packets, a.steps, a.warmup, rank, world, dist, local)
     flen = res["flen"]
+    bpl = res["bytes_per_launch"]  # frame bytes one launch builds on one GPU
     pkts_total = a.packets * a.steps * world
     wall = res["wall_s"]
     mpps = pkts_total / wall / 1e6
-    gbps = pkts_total * flen / wall / 1e9
+    gbps = bpl * a.steps * world / wall / 1e9
     k_s = res["kernel_ms_avg"] * 1e-3
-    achieved = a.packets * flen / k_s / 1e9
+    achieved = bpl / k_s / 1e9
     extra = {}
+    peak_probe = None
+    if rank == 0:
+        fill_ms = ctx.fill_probe(bpl, 20)
+        peak_probe = bpl / (fill_ms * 1e-3) / 1e9
+        extra["write_peak_probe_gbps"] = round(peak_probe, 1)
     if not a.no_variants:
-        v = run_config(ctx, "c2_udp_1500", 1, a.packets, max(3, a.steps // 4), 1, rank, world, dist, local)
-        n1500 = a.packets * max(3, a.steps // 4) * world
+        steps15 = max(3, a.steps // 4)
+        v = run_config(ctx, "c2_udp_1500", 1, a.packets, steps15, 1, rank, world, dist, local)
+        n1500 = a.packets * steps15 * world
+        ach15 = v["bytes_per_launch"] / (v["kernel_ms_avg"] * 1e-3) / 1e9
         extra["udp_1500"] = {
-            "mpps": n1500 / v["wall_s"] / 1e6, "gbps": n1500 * v["flen"] / v["wall_s"] / 1e9,
-            "kernel_ms_avg": v["kernel_ms_avg"],
-            "roofline_frac": a.packets * v["flen"] / (v["kernel_ms_avg"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "mpps": round(n1500 / v["wall_s"] / 1e6, 3),
+            "gbps": round(v["bytes_per_launch"] * steps15 * world / v["wall_s"] / 1e9, 2),
+            "kernel": v["kernel"], "kernel_ms_avg": round(v["kernel_ms_avg"], 4),
+            "roofline_achieved_gbps": round(ach15, 1), "roofline_frac": round(ach15 / HBM_PEAK_GBPS, 4),
             "packets_per_launch": a.packets}
         if rank == 0:
-            fill_ms = ctx.fill_probe(a.packets * flen, 20)
-            extra["write_peak_probe_gbps"] = a.packets * flen / (fill_ms * 1e-3) / 1e9
             extra["d2h_umem_64B"] = d2h_rate(ctx, 0, a.packets)
     ctx.close()
     if rank != 0:
@@ -204,14 +215,16 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seed stream splitmix64(0x5EEDBA5E ^ (seq<<48) + k); SURVEY.md §8d C2)",
-        "config": {"workload": "configs[1] UDP 64B frame, 10.20.0.0/16 random src + random sport, 22-B random "
-                               "payload, L3+L4 checksums", "packets_per_launch_per_gpu": a.packets,
-                   "frame_bytes": flen, "parallelism": f"shard-by-iteration x{world}"},
+        "config": {"workload": f"{a.config}: " + " ".join((pc.BASELINE.get(a.config) or pc.c2_udp_64).__doc__.split()),
+                   "packets_per_launch_per_gpu": a.packets,
+                   "frame_bytes": flen or None, "bytes_per_launch_per_gpu": bpl,
+                   "parallelism": f"shard-by-iteration x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": pmc_traffic(a.pmc, a.config), "kernel": "pb_build_kernel<true>",
+                     "traffic": pmc_traffic(a.pmc, a.config), "kernel": res["kernel"],
                      "kernel_ms_avg": round(res["kernel_ms_avg"], 5),
-                     "algorithmic_bytes_per_launch": a.packets * flen},
+                     "algorithmic_bytes_per_launch": bpl,
+                     "frac_of_measured_write_peak": round(achieved / peak_probe, 4) if peak_probe else None},
     }
     if res["counters"] is not None:
         line["global_counters"] = {"packets": res["counters"][0], "bytes": res["counters"][1]}

@@ -132,6 +132,10 @@ int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_p
 /* Build-kernel tile size chosen for a sequence (bytes per workgroup). */
 int pbgpu_tile_bytes(pbgpu_ctx *ctx, uint16_t seq_idx, uint32_t *tile_bytes);
 
+/* Name of the frame-build kernel variant a loaded sequence launches
+ * (as rocprofv3 reports it). */
+int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n);
+
 /* ABI self-description for FFI bindings: sizes / offsets of the structs above.
  * which: 0 sizeof(pb_sequence_t), 1 sizeof(pb_payload_opt_t), 2 sizeof(pbgpu_frames),
  *        3 offsetof(pb_sequence_t, ip.ranges), 4 offsetof(pb_sequence_t, pls),

@@ -695,12 +695,49 @@ __device__ __forceinline__ void pb_store_chunk(uint8_t *p, uint32_t o0, uint32_t
     }
 }
 
+// 16 payload bytes starting at payload index j0 of a frame (random: from LCG
+// state x for j0; static: blob bytes at src + j0), bytes outside [lo, hi) zeroed
+__device__ __forceinline__ void pb_chunk_payload(const pb_kargs &K, bool rnd, uint32_t x, uint32_t src, int j0, int lo,
+                                                 int hi, uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3)
+{
+    const uint32_t a3 = PB_A3, c3 = PB_C3;
+    if (rnd)
+    {
+        uint32_t x0 = x, x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+        o0 = pb_pack4(x0, x1, x2, x3);
+        x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+        o1 = pb_pack4(x0, x1, x2, x3);
+        x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+        o2 = pb_pack4(x0, x1, x2, x3);
+        x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+        o3 = pb_pack4(x0, x1, x2, x3);
+    }
+    else
+    {
+        const uint8_t *bp = K.blob + src + j0;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)bp & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)((uintptr_t)bp & 3);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+        o0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        o1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        o2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        o3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
+    }
+    if (lo > 0 || hi < 16)
+    {
+        o0 &= pb_range_mask(lo, hi);
+        o1 &= pb_range_mask(lo - 4, hi - 4);
+        o2 &= pb_range_mask(lo - 8, hi - 8);
+        o3 &= pb_range_mask(lo - 12, hi - 12);
+    }
+}
+
 template <int G>
 __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_img[PB_WG * PB_IMG_STRIDE];
-    __shared__ uint32_t s_blo[PB_WG], s_bhi[PB_WG], s_flen[PB_WG], s_z[PB_WG], s_nv[PB_WG], s_src[PB_WG],
-        s_hsum[PB_WG];
+    __shared__ uint32_t s_blo[PB_WG], s_bhi[PB_WG], s_flen[PB_WG], s_z[PB_WG], s_st0[PB_WG], s_nv[PB_WG],
+        s_src[PB_WG], s_hsum[PB_WG];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t flags = K.flags;
@@ -745,13 +782,13 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
         row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
         row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
         row[4] = pb_u32x4{0u, 0u, 0u, 0u};
-        // LCG state for the payload byte at the first chunk's first position:
-        // j = -(base % 16 + hl), i.e. L^(3(1 - base % 16 - hl))(st0)
+        // LCG state for payload index j = -(base % 16 + hl), the first chunk's first byte
         const uint2 jt = K.jump[PB_JNEG - ((uint32_t)(base & 15u) + (uint32_t)hl)];
         s_blo[tid] = (uint32_t)base;
         s_bhi[tid] = (uint32_t)(base >> 32);
         s_flen[tid] = flen;
         s_z[tid] = P.random ? jt.x * P.st0 + jt.y : 0u;
+        s_st0[tid] = P.st0;
         s_nv[tid] = P.nvalid | (P.random << 31);
         s_src[tid] = P.blob_off;
         s_hsum[tid] = hs;
@@ -763,7 +800,6 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
     const uint32_t lane = tid & 63u, wave = tid >> 6;
     const uint32_t g = lane / G, lg = lane % G;
     const uint2 Ml = K.lcg48[lg], MG = K.lcg48[G];
-    const uint32_t a3 = PB_A3, c3 = PB_C3;
     const uint32_t nt = K.nt_stores;
 
     for (uint32_t p = 0; p < 64 / NG; ++p)
@@ -780,70 +816,97 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
         const int nvalid = (int)(nv & 0x7FFFFFFFu);
         const uint32_t src = s_src[fr];
         uint8_t *const out = K.out + (base & ~15ull);
+        // Frame edges.  The 16-B chunk shared with the previous frame is stored whole
+        // by this frame's chunk-0 lane, which also generates the previous frame's
+        // payload tail for it (cov_in); symmetrically this frame does not store its
+        // last chunk when the next frame covers it (cov_out).  Needs the neighbour in
+        // this workgroup and its bytes in that chunk to be payload, not header.
+        const int e = (s0 + flen) & 15;
+        const bool cov_in = s0 != 0 && fr > 0 && (int)s_flen[fr - 1] - hl >= s0;
+        const bool cov_out = e != 0 && fr + 1 < nfr && flen - hl >= e;
         uint32_t x = __umul24(s_z[fr], Ml.x) + Ml.y;
-        uint32_t acc = 0;
-        uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-        int hq = 0;
-        bool held = false;
+        unsigned long long acc = 0;
 
+        // interior chunks (all 16 bytes drawn payload): generate, sum, store.  Edge
+        // chunks (header bytes, or the end of the drawn payload) are kept for later.
+        int eq0 = 0, eq1 = 0;
+        uint32_t ex0 = 0, ex1 = 0;
+        uint32_t ne = 0;
         for (uint32_t m = lg; m < nch; m += G)
         {
             const int q0 = (int)(16 * m) - s0; // frame position of the chunk's first byte
             const int j0 = q0 - hl;            // payload index of the chunk's first byte
-            uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
-            if (j0 < nvalid && j0 + 16 > 0)
+            if (j0 >= 0 && j0 + 16 <= nvalid)
             {
+                uint32_t o0, o1, o2, o3;
+                pb_chunk_payload(K, rnd, x, src, j0, 0, 16, o0, o1, o2, o3);
                 if (rnd)
-                {
-                    uint32_t x0 = x, x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
-                    o0 = pb_pack4(x0, x1, x2, x3);
-                    x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
-                    o1 = pb_pack4(x0, x1, x2, x3);
-                    x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
-                    o2 = pb_pack4(x0, x1, x2, x3);
-                    x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
-                    o3 = pb_pack4(x0, x1, x2, x3);
-                }
+                    acc += (unsigned long long)o0 + o1 + o2 + o3;
+                if (nt)
+                    __builtin_nontemporal_store(pb_u32x4{o0, o1, o2, o3}, reinterpret_cast<pb_u32x4 *>(out + 16 * m));
                 else
-                {
-                    const uint8_t *bp = K.blob + src + j0;
-                    const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)bp & ~(uintptr_t)3);
-                    const uint32_t sh = (uint32_t)((uintptr_t)bp & 3);
-                    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-                    o0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-                    o1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-                    o2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-                    o3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
-                }
-                const int lo = -j0, hi = nvalid - j0; // valid payload bytes of the chunk: [lo, hi)
-                if (lo > 0 || hi < 16)
-                {
-                    o0 &= pb_range_mask(lo, hi);
-                    o1 &= pb_range_mask(lo - 4, hi - 4);
-                    o2 &= pb_range_mask(lo - 8, hi - 8);
-                    o3 &= pb_range_mask(lo - 12, hi - 12);
-                }
-                if (rnd)
-                    acc += pb_halves(o0) + pb_halves(o1) + pb_halves(o2) + pb_halves(o3);
+                    *reinterpret_cast<pb_u32x4 *>(out + 16 * m) = pb_u32x4{o0, o1, o2, o3};
             }
-            if (q0 < hl)
+            else if (j0 >= nvalid && j0 >= 0)
             {
-                h0 = o0, h1 = o1, h2 = o2, h3 = o3;
-                hq = q0;
-                held = true;
+                // past the drawn bytes (literal rule): zeros up to the frame end
+                if (!(m + 1 == nch && cov_out))
+                    pb_store_chunk(out + 16 * m, 0u, 0u, 0u, 0u, q0, flen, nt);
             }
             else
             {
-                pb_store_chunk(out + 16 * m, o0, o1, o2, o3, q0, flen, nt);
+                if (ne == 0)
+                    eq0 = q0, ex0 = x;
+                else
+                    eq1 = q0, ex1 = x;
+                ++ne;
             }
             x = __umul24(x, MG.x) + MG.y;
         }
+
+        // edge chunks: at most two per lane (a head chunk in the first step, a tail chunk)
+        uint32_t eo[2][4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+        {
+            eo[i][0] = eo[i][1] = eo[i][2] = eo[i][3] = 0u;
+            if ((uint32_t)i < ne)
+            {
+                const int q0 = i ? eq1 : eq0;
+                bool grnd = rnd;
+                uint32_t gx = i ? ex1 : ex0, gsrc = src;
+                int j0 = q0 - hl, lo = -j0, hi = nvalid - j0;
+                const bool special = q0 == -s0 && cov_in; // chunk 0 shared with the previous frame
+                if (special)
+                {
+                    // the previous frame's last payload bytes fill chunk bytes [0, s0)
+                    const int pf = (int)s_flen[fr - 1];
+                    const uint32_t pnv = s_nv[fr - 1];
+                    grnd = (pnv >> 31) != 0;
+                    j0 = pf - s0 - hl;
+                    lo = 0;
+                    hi = min((int)(pnv & 0x7FFFFFFFu) - j0, s0);
+                    gsrc = s_src[fr - 1];
+                    const uint2 jt = K.jump[(uint32_t)j0 + PB_JNEG];
+                    gx = grnd ? jt.x * s_st0[fr - 1] + jt.y : 0u;
+                }
+                if (lo < 16 && hi > 0 && lo < hi)
+                {
+                    pb_chunk_payload(K, grnd, gx, gsrc, j0, lo, hi, eo[i][0], eo[i][1], eo[i][2], eo[i][3]);
+                    if (grnd && !special)
+                        acc += (unsigned long long)eo[i][0] + eo[i][1] + eo[i][2] + eo[i][3];
+                }
+            }
+        }
+
+        // one's complement sum of 32-bit words == sum of their 16-bit halves (mod 0xFFFF)
+        uint32_t sum = pb_halves((uint32_t)acc) + pb_halves((uint32_t)(acc >> 32));
 #pragma unroll
         for (int w = 1; w < G; w <<= 1)
-            acc += __shfl_xor(acc, w, 64);
+            sum += __shfl_xor(sum, w, 64);
         if ((flags & PBK_L4_CSUM) && lg == 0)
         {
-            uint32_t pc = pb_fold(acc);
+            uint32_t pc = pb_fold(sum);
             if (base & 1u) // chunk sums were taken in output alignment
                 pc = pb_bswap16(pc);
             const uint32_t c = (~pb_fold(pb_fold(s_hsum[fr]) + pc)) & 0xFFFFu;
@@ -851,14 +914,26 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        if (held)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
         {
-            const uint32_t *img = s_img + fr * PB_IMG_STRIDE;
-            h0 |= pb_window(img, hq);
-            h1 |= pb_window(img, hq + 4);
-            h2 |= pb_window(img, hq + 8);
-            h3 |= pb_window(img, hq + 12);
-            pb_store_chunk(out + (hq + s0), h0, h1, h2, h3, hq, flen, nt);
+            if ((uint32_t)i < ne)
+            {
+                const int q0 = i ? eq1 : eq0;
+                const uint32_t m = (uint32_t)(q0 + s0) >> 4;
+                uint32_t o0 = eo[i][0], o1 = eo[i][1], o2 = eo[i][2], o3 = eo[i][3];
+                if (q0 < hl)
+                {
+                    const uint32_t *img = s_img + fr * PB_IMG_STRIDE;
+                    o0 |= pb_window(img, q0);
+                    o1 |= pb_window(img, q0 + 4);
+                    o2 |= pb_window(img, q0 + 8);
+                    o3 |= pb_window(img, q0 + 12);
+                }
+                const bool special = q0 == -s0 && cov_in; // holds the previous frame's tail too: store whole
+                if (!(m + 1 == nch && cov_out))
+                    pb_store_chunk(out + 16 * m, o0, o1, o2, o3, special ? 0 : q0, special ? 16 : flen, nt);
+            }
         }
     }
     if (K.fixed_len && blockIdx.x == 0 && tid == 0)
@@ -990,11 +1065,24 @@ __global__ __launch_bounds__(64) void pb_scatter_slots(const uint8_t *src, const
         d[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
 
+// write-only roofline probe: each workgroup streams 16 KiB as 4 contiguous
+// 4-KiB sweeps of 16-B stores (the store shape of the build kernels)
+template <bool NT>
 __global__ __launch_bounds__(256) void pb_fill_kernel(pb_u32x4 *dst, uint64_t n16, uint32_t v)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
-        __builtin_nontemporal_store(pb_u32x4{v, v ^ (uint32_t)i, v, (uint32_t)i}, dst + i);
+    const uint64_t b = (uint64_t)blockIdx.x * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+    {
+        const uint64_t c = b + i * 256 + threadIdx.x;
+        if (c < n16)
+        {
+            if (NT)
+                __builtin_nontemporal_store(pb_u32x4{v, v ^ (uint32_t)c, v, (uint32_t)c}, dst + c);
+            else
+                dst[c] = pb_u32x4{v, v ^ (uint32_t)c, v, (uint32_t)c};
+        }
+    }
 }
 
 // ---------------- launch wrappers (called from pbgpu.cpp) ----------------
@@ -1063,9 +1151,13 @@ extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *off
     return hipGetLastError();
 }
 
-extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, hipStream_t st)
+extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int nt, hipStream_t st)
 {
     const uint64_t n16 = bytes / 16;
-    hipLaunchKernelGGL(pb_fill_kernel, dim3(256 * 8), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+    const uint32_t grid = (uint32_t)((n16 + 1023) / 1024);
+    if (nt)
+        hipLaunchKernelGGL(pb_fill_kernel<true>, dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+    else
+        hipLaunchKernelGGL(pb_fill_kernel<false>, dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
     return hipGetLastError();
 }

@@ -285,6 +285,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pbgpu_fill_probe": (C.c_int, [P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
         "pbgpu_tile_bytes": (C.c_int, [P, C.c_uint16, C.POINTER(C.c_uint32)]),
         "pbgpu_abi_size": (C.c_size_t, [C.c_int]),
+        "pbgpu_kernel_name": (C.c_int, [P, C.c_uint16, C.c_char_p, C.c_size_t]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -419,6 +420,11 @@ class GpuContext:
         t = C.c_uint32()
         _check(self.lib.pbgpu_tile_bytes(self.h, idx, C.byref(t)), "tile_bytes")
         return int(t.value)
+
+    def kernel_name(self, idx: int) -> str:
+        buf = C.create_string_buffer(96)
+        _check(self.lib.pbgpu_kernel_name(self.h, idx, buf, 96), "kernel_name")
+        return buf.value.decode()
 
     def build_frames(self, idx: int, first_iter: int, n_iter: int) -> list:
         """Convenience: build into a fresh buffer and return the frames as bytes."""
