@@ -92,6 +92,7 @@ struct pb_kargs
     unsigned long long *counters; // [2] pckts, bytes of this sequence
     uint32_t small_ndw;     // >0: small fixed frames, one lane per frame, NDW dwords per lane
     uint32_t gpf_g;         // >0: group-per-frame kernel with G lanes per frame
+    uint32_t gpf_rmode;     // 1: all payloads random, 0: all static, 2: mixed
     const uint2 *lcg48;     // lcg48[m] = L^(48 m): one 16-B chunk of payload = 48 LCG steps
     uint32_t nt_stores;     // 1: non-temporal output stores
     uint32_t stail[32];     // small kernel, static payload: payload bytes at frame dwords p0.. (p0 = (hl-2)/4)
@@ -140,4 +141,13 @@ __device__ __forceinline__ uint32_t pb_fold(uint32_t s)
 __device__ __forceinline__ uint32_t pb_halves(uint32_t d)
 {
     return (d & 0xFFFFu) + (d >> 16);
+}
+
+typedef unsigned short pb_u16x2 __attribute__((ext_vector_type(2)));
+
+// acc + low16(d) + high16(d) in one v_dot2_u32_u16
+__device__ __forceinline__ uint32_t pb_add_halves(uint32_t acc, uint32_t d)
+{
+    const pb_u16x2 one = {1, 1};
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(pb_u16x2, d), one, acc, false);
 }

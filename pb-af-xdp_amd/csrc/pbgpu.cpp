@@ -644,7 +644,32 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         if (tile)
             K.small_ndw = 0;
         else if (!K.small_ndw)
-            K.gpf_g = maxf <= 320 ? 8 : 32;
+        {
+            // lanes per frame (measured, profiles/r01/gsweep): equal-length frames take
+            // the group size that wastes the fewest lanes on the frame's chunk count,
+            // preferring 32 (1500-B frames: 4.2 TB/s at G=32, 3.5 at 8, 2.9 at 64);
+            // packed variable-length frames take 8 (configs[2]: 3.35 TB/s at 8, 2.7
+            // at 32).  PBGPU_G overrides (8, 16, 32, 64) for experiments.
+            if (K.fixed_len)
+            {
+                const uint32_t nch = (minf + 15) / 16 + 1;
+                double best = -1;
+                for (uint32_t gg : {32u, 16u, 8u})
+                {
+                    const double util = (double)nch / (gg * ((nch + gg - 1) / gg));
+                    if (util > best + 0.05)
+                        best = util, K.gpf_g = gg;
+                }
+            }
+            else
+            {
+                K.gpf_g = 8;
+            }
+            const char *ge = getenv("PBGPU_G");
+            if (ge && (atoi(ge) == 8 || atoi(ge) == 16 || atoi(ge) == 32 || atoi(ge) == 64))
+                K.gpf_g = (uint32_t)atoi(ge);
+            K.gpf_rmode = n_random == (int)pls.size() ? 1 : (n_random == 0 ? 0 : 2);
+        }
     }
     // tile: power of two, <= 16 KiB, <= (PB_NF_MAX - 2) frames of minimum length
     uint32_t cap = (PB_NF_MAX - 2) * minf;
@@ -1052,9 +1077,9 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         return PBGPU_ENOENT;
     const pb_kargs &K = S.K;
     if (K.gpf_g)
-        snprintf(buf, n, "pb_gpf_kernel<%u>", K.gpf_g);
+        snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.small_ndw)
-        snprintf(buf, n, "pb_small_kernel<%u,%u,%s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
+        snprintf(buf, n, "pb_small_kernel<%u, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
     else
         snprintf(buf, n, "pb_build_kernel<%s>", K.fixed_len ? "true" : "false");
     return PBGPU_OK;

@@ -557,7 +557,7 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
         uint32_t sum = d[8] >> 16;
 #pragma unroll
         for (int t = 9; t < NDW; ++t)
-            sum += pb_halves(d[t]);
+            sum = pb_add_halves(sum, d[t]);
         if (PROTO != 1)
             sum += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((PROTO + l4tot) << 8);
         const uint32_t c = (flags & PBK_L4_CSUM) ? ((~pb_fold(sum)) & 0xFFFFu) : 0u;
@@ -732,7 +732,8 @@ __device__ __forceinline__ void pb_chunk_payload(const pb_kargs &K, bool rnd, ui
     }
 }
 
-template <int G>
+// RMODE: 1 every payload random, 0 every payload static, 2 mixed (multi-payload)
+template <int G, int RMODE>
 __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_img[PB_WG * PB_IMG_STRIDE];
@@ -812,7 +813,7 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
         const int s0 = (int)(base & 15u);
         const uint32_t nch = (uint32_t)(s0 + flen + 15) >> 4;
         const uint32_t nv = s_nv[fr];
-        const bool rnd = (nv >> 31) != 0;
+        const bool rnd = RMODE == 2 ? (nv >> 31) != 0 : RMODE == 1;
         const int nvalid = (int)(nv & 0x7FFFFFFFu);
         const uint32_t src = s_src[fr];
         uint8_t *const out = K.out + (base & ~15ull);
@@ -825,7 +826,7 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
         const bool cov_in = s0 != 0 && fr > 0 && (int)s_flen[fr - 1] - hl >= s0;
         const bool cov_out = e != 0 && fr + 1 < nfr && flen - hl >= e;
         uint32_t x = __umul24(s_z[fr], Ml.x) + Ml.y;
-        unsigned long long acc = 0;
+        uint32_t acc = 0;
 
         // interior chunks (all 16 bytes drawn payload): generate, sum, store.  Edge
         // chunks (header bytes, or the end of the drawn payload) are kept for later.
@@ -841,7 +842,7 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
                 uint32_t o0, o1, o2, o3;
                 pb_chunk_payload(K, rnd, x, src, j0, 0, 16, o0, o1, o2, o3);
                 if (rnd)
-                    acc += (unsigned long long)o0 + o1 + o2 + o3;
+                    acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
                 if (nt)
                     __builtin_nontemporal_store(pb_u32x4{o0, o1, o2, o3}, reinterpret_cast<pb_u32x4 *>(out + 16 * m));
                 else
@@ -882,7 +883,7 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
                     // the previous frame's last payload bytes fill chunk bytes [0, s0)
                     const int pf = (int)s_flen[fr - 1];
                     const uint32_t pnv = s_nv[fr - 1];
-                    grnd = (pnv >> 31) != 0;
+                    grnd = RMODE == 2 ? (pnv >> 31) != 0 : RMODE == 1;
                     j0 = pf - s0 - hl;
                     lo = 0;
                     hi = min((int)(pnv & 0x7FFFFFFFu) - j0, s0);
@@ -894,13 +895,13 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
                 {
                     pb_chunk_payload(K, grnd, gx, gsrc, j0, lo, hi, eo[i][0], eo[i][1], eo[i][2], eo[i][3]);
                     if (grnd && !special)
-                        acc += (unsigned long long)eo[i][0] + eo[i][1] + eo[i][2] + eo[i][3];
+                        acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, eo[i][0]), eo[i][1]), eo[i][2]),
+                                            eo[i][3]);
                 }
             }
         }
 
-        // one's complement sum of 32-bit words == sum of their 16-bit halves (mod 0xFFFF)
-        uint32_t sum = pb_halves((uint32_t)acc) + pb_halves((uint32_t)(acc >> 32));
+        uint32_t sum = acc;
 #pragma unroll
         for (int w = 1; w < G; w <<= 1)
             sum += __shfl_xor(sum, w, 64);
@@ -1112,10 +1113,33 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid,
     if (K->gpf_g)
     {
         const uint32_t grid = (uint32_t)((K->n_frames + PB_WG - 1) / PB_WG);
+        const uint32_t rm = K->gpf_rmode;
+#define PB_GPF(GG, RM) hipLaunchKernelGGL((pb_gpf_kernel<GG, RM>), dim3(grid), dim3(PB_WG), 0, st, *K)
+#define PB_GPF_RM(GG)      \
+    if (rm == 1)           \
+        PB_GPF(GG, 1);     \
+    else if (rm == 0)      \
+        PB_GPF(GG, 0);     \
+    else                   \
+        PB_GPF(GG, 2)
         if (K->gpf_g == 8)
-            hipLaunchKernelGGL((pb_gpf_kernel<8>), dim3(grid), dim3(PB_WG), 0, st, *K);
+        {
+            PB_GPF_RM(8);
+        }
+        else if (K->gpf_g == 16)
+        {
+            PB_GPF_RM(16);
+        }
+        else if (K->gpf_g == 32)
+        {
+            PB_GPF_RM(32);
+        }
         else
-            hipLaunchKernelGGL((pb_gpf_kernel<32>), dim3(grid), dim3(PB_WG), 0, st, *K);
+        {
+            PB_GPF_RM(64);
+        }
+#undef PB_GPF_RM
+#undef PB_GPF
     }
     else if (K->small_ndw)
     {
