@@ -29,6 +29,7 @@ for _p in (ROOT, PKG, os.path.join(ROOT, "tests")):
 import numpy as np  # noqa: E402
 
 import pb_configs as pc  # noqa: E402
+import pb_dist  # noqa: E402
 from pbgpu import GpuContext, Sequence  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -77,7 +78,7 @@ def run_config(ctx, name, seq_idx, n_pkts, steps, warmup, rank, world, dist, loc
     seq = Sequence.from_config(pc.get(name))
     ctx.load_sequence(seq_idx, seq, pc.SEED_BASE)
     fb = ctx.alloc_frames(*ctx.build_size(seq_idx, n_pkts))
-    step_iter = lambda s: (s * world + rank) * n_pkts  # disjoint per rank and step  # noqa: E731
+    step_iter = lambda s: pb_dist.step_first_iter(s, rank, world, n_pkts)  # noqa: E731
     for s in range(warmup):
         ctx.build(seq_idx, step_iter(s), n_pkts, fb)
     ctx.sync()
@@ -90,12 +91,10 @@ def run_config(ctx, name, seq_idx, n_pkts, steps, warmup, rank, world, dist, loc
     ctx.sync()
     counters = None
     if dist is not None:
-        import torch
-
         p, b = ctx.counters(seq_idx + 1)
-        t = torch.tensor([int(p[seq_idx]), int(b[seq_idx])], dtype=torch.int64, device=f"cuda:{local}")
-        dist.all_reduce(t)  # RCCL over xGMI: the global sent-packet / byte counter
-        counters = t.tolist()
+        # RCCL over xGMI: the global sent-packet / byte counter
+        gp, gb = pb_dist.allreduce_counters([p[seq_idx]], [b[seq_idx]], device=f"cuda:{local}")
+        counters = [gp[0], gb[0]]
     barrier(dist, local)
     wall = time.perf_counter() - t0
     k_ms, k_n = ctx.kernel_time()

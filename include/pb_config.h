@@ -105,6 +105,13 @@ typedef struct pb_sequence
     uint16_t pl_cnt;
 } pb_sequence_t;
 
+/* PB-Common config_t (main.c:65-94 fills it): the interface and the sequences. */
+typedef struct pb_config
+{
+    const char *interface;
+    pb_sequence_t seq[PB_MAX_SEQUENCES];
+} pb_config_t;
+
 /* Declared rules for the reference quirks that are not pinned by any
  * reference fixture (DESIGN.md "Declared rules"). */
 enum pb_payload_rule

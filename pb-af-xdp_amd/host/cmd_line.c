@@ -1,0 +1,112 @@
+/*
+ * cmd_line.c — AF_XDP + GPU command-line parsing (see cmd_line.h).
+ * Reference behaviour kept: getopt_long with no short options, codes 1-7 for
+ * queue / nowakeup / sharedumem / batchsize / skb / zerocopy / copy, values
+ * through atoi (src/cmd_line.c:24-69); unknown options are skipped silently
+ * (main.c sets opterr = 0 before the passes).
+ */
+#include "cmd_line.h"
+
+#include <getopt.h>
+#include <stdlib.h>
+
+enum
+{
+    OPT_QUEUE = 1,
+    OPT_NOWAKEUP,
+    OPT_SHAREDUMEM,
+    OPT_BATCHSIZE,
+    OPT_SKB,
+    OPT_ZEROCOPY,
+    OPT_COPY,
+    OPT_GPUS = 32,
+    OPT_GPU,
+    OPT_GPUBATCH,
+    OPT_SEED,
+    OPT_LITERAL,
+    OPT_SINGLEFOLD,
+    OPT_PCAP,
+};
+
+static const struct option af_xdp_opts[] = {
+    {"queue", required_argument, NULL, OPT_QUEUE},
+    {"nowakeup", no_argument, NULL, OPT_NOWAKEUP},
+    {"sharedumem", no_argument, NULL, OPT_SHAREDUMEM},
+    {"batchsize", required_argument, NULL, OPT_BATCHSIZE},
+    {"skb", no_argument, NULL, OPT_SKB},
+    {"zerocopy", no_argument, NULL, OPT_ZEROCOPY},
+    {"copy", no_argument, NULL, OPT_COPY},
+    {"gpus", required_argument, NULL, OPT_GPUS},
+    {"gpu", required_argument, NULL, OPT_GPU},
+    {"gpubatch", required_argument, NULL, OPT_GPUBATCH},
+    {"seed", required_argument, NULL, OPT_SEED},
+    {"literal", no_argument, NULL, OPT_LITERAL},
+    {"singlefold", no_argument, NULL, OPT_SINGLEFOLD},
+    {"pcap", required_argument, NULL, OPT_PCAP},
+    {NULL, 0, NULL, 0},
+};
+
+void cmd_line_af_xdp_defaults(struct cmd_line_af_xdp *c)
+{
+    c->batch_size = 1; /* main.c:45-46 */
+    c->gpus = 1;
+    c->gpu_first = 0;
+    c->gpu_batch = 1u << 20;
+    c->seed_base = 0x5EEDBA5Eull;
+}
+
+void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *c, int argc, char **argv)
+{
+    int opt;
+    while ((opt = getopt_long(argc, argv, "", af_xdp_opts, NULL)) != -1)
+    {
+        switch (opt)
+        {
+        case OPT_QUEUE:
+            c->queue_set = 1;
+            c->queue = atoi(optarg);
+            break;
+        case OPT_NOWAKEUP:
+            c->no_wake_up = 1;
+            break;
+        case OPT_SHAREDUMEM:
+            c->shared_umem = 1;
+            break;
+        case OPT_BATCHSIZE:
+            c->batch_size = (unsigned short)atoi(optarg);
+            break;
+        case OPT_SKB:
+            c->skb_mode = 1;
+            break;
+        case OPT_ZEROCOPY:
+            c->zero_copy = 1;
+            break;
+        case OPT_COPY:
+            c->copy = 1;
+            break;
+        case OPT_GPUS:
+            c->gpus = atoi(optarg);
+            break;
+        case OPT_GPU:
+            c->gpu_first = atoi(optarg);
+            break;
+        case OPT_GPUBATCH:
+            c->gpu_batch = strtoull(optarg, NULL, 0);
+            break;
+        case OPT_SEED:
+            c->seed_base = strtoull(optarg, NULL, 0);
+            break;
+        case OPT_LITERAL:
+            c->literal_payload = 1;
+            break;
+        case OPT_SINGLEFOLD:
+            c->single_fold = 1;
+            break;
+        case OPT_PCAP:
+            c->pcap = optarg;
+            break;
+        default:
+            break;
+        }
+    }
+}

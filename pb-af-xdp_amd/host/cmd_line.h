@@ -1,0 +1,37 @@
+/*
+ * cmd_line.h — AF_XDP command-line surface of pcktbatch, extended with the
+ * GPU options of this build.
+ *
+ * The first fields mirror the reference's struct cmd_line_af_xdp
+ * (src/cmd_line.h:7-18) member for member, and parse_cmd_line_af_xdp() keeps
+ * its getopt_long table (codes 1-7, src/cmd_line.c:3-13) and behaviour, so a
+ * reference command line parses identically.  GPU options use codes >= 32.
+ */
+#pragma once
+
+#include <stdint.h>
+
+typedef struct cmd_line_af_xdp
+{
+    unsigned int queue_set : 1;
+    int queue;
+
+    unsigned int no_wake_up : 1;
+    unsigned int shared_umem;
+    unsigned short batch_size;
+    unsigned int skb_mode : 1;
+    unsigned int zero_copy : 1;
+    unsigned int copy : 1;
+
+    /* GPU options (this build) */
+    int gpus;            /* --gpus N: GPUs per sequence (default 1) */
+    int gpu_first;       /* --gpu I: first GPU index (default 0) */
+    uint64_t gpu_batch;  /* --gpubatch K: iterations per GPU launch (default 1 << 20) */
+    uint64_t seed_base;  /* --seed S: seed stream base (default 0x5EEDBA5E) */
+    int literal_payload; /* --literal: reference's as-compiled payload loop (quirk B1) */
+    int single_fold;     /* --singlefold: one-fold IPv4 checksum (quirk B6) */
+    const char *pcap;    /* --pcap FILE: write built frames to a pcap file */
+} cmd_line_af_xdp_t;
+
+void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *cmd_af_xdp, int argc, char **argv);
+void cmd_line_af_xdp_defaults(struct cmd_line_af_xdp *cmd_af_xdp);

@@ -1,0 +1,232 @@
+/*
+ * main_gpu.c — pcktbatch-gpu: the reference's program entry (src/main.c)
+ * with the packet build on MI355X.
+ *
+ * Same two-pass command line as main.c:23-94 (opterr = 0; common options,
+ * then optind = 0 and the AF_XDP options of cmd_line.c plus this build's GPU
+ * options), the first-sequence override (-z, README.md:101-151), sequences
+ * run in order through seq_send(), shutdown_prog() on exit or SIGINT/SIGTERM.
+ * JSON config files (-c) need PB-Common + json-c, which are not in this
+ * build: use -z, or the Python loader (pb-af-xdp_amd/pbgpu.py).
+ * Frames go to the TX hook: a pcap file with --pcap, otherwise counted.
+ */
+#include <getopt.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "cmd_line.h"
+#include "sequence_gpu.h"
+
+typedef struct cmd_line
+{
+    const char *config;
+    int cli, list, verbose, help;
+} cmd_line_t;
+
+static pb_config_t *cfg;
+
+static void sign_hdl(int sig)
+{
+    (void)sig;
+    pb_request_stop();
+}
+
+enum
+{
+    O_INTERFACE = 256, O_BLOCK, O_TRACK, O_MAXPCKTS, O_MAXBYTES, O_PPS, O_BPS, O_DELAY, O_THREADS, O_L4CSUM, O_SMAC,
+    O_DMAC, O_MINTTL, O_MAXTTL, O_MINID, O_MAXID, O_SIP, O_DIP, O_PROTOCOL, O_TOS, O_L3CSUM, O_USPORT, O_UDPORT,
+    O_TSPORT, O_TDPORT, O_SYN, O_ACK, O_PSH, O_RST, O_FIN, O_URG, O_ECE, O_CWR, O_PMIN, O_PMAX, O_PSTATIC, O_PEXACT,
+    O_PFILE, O_PSTRING, O_TIME,
+};
+
+static const struct option common_opts[] = {
+    {"cfg", required_argument, NULL, 'c'},   {"list", no_argument, NULL, 'l'},
+    {"verbose", no_argument, NULL, 'v'},     {"help", no_argument, NULL, 'h'},
+    {"cli", no_argument, NULL, 'z'},         {"interface", required_argument, NULL, O_INTERFACE},
+    {"block", required_argument, NULL, O_BLOCK}, {"track", required_argument, NULL, O_TRACK},
+    {"maxpckts", required_argument, NULL, O_MAXPCKTS}, {"maxbytes", required_argument, NULL, O_MAXBYTES},
+    {"pps", required_argument, NULL, O_PPS}, {"bps", required_argument, NULL, O_BPS},
+    {"delay", required_argument, NULL, O_DELAY}, {"threads", required_argument, NULL, O_THREADS},
+    {"l4csum", required_argument, NULL, O_L4CSUM}, {"smac", required_argument, NULL, O_SMAC},
+    {"dmac", required_argument, NULL, O_DMAC}, {"minttl", required_argument, NULL, O_MINTTL},
+    {"maxttl", required_argument, NULL, O_MAXTTL}, {"minid", required_argument, NULL, O_MINID},
+    {"maxid", required_argument, NULL, O_MAXID}, {"sip", required_argument, NULL, O_SIP},
+    {"dip", required_argument, NULL, O_DIP}, {"protocol", required_argument, NULL, O_PROTOCOL},
+    {"tos", required_argument, NULL, O_TOS}, {"l3csum", required_argument, NULL, O_L3CSUM},
+    {"usport", required_argument, NULL, O_USPORT}, {"udport", required_argument, NULL, O_UDPORT},
+    {"tsport", required_argument, NULL, O_TSPORT}, {"tdport", required_argument, NULL, O_TDPORT},
+    {"syn", required_argument, NULL, O_SYN}, {"ack", required_argument, NULL, O_ACK},
+    {"psh", required_argument, NULL, O_PSH}, {"rst", required_argument, NULL, O_RST},
+    {"fin", required_argument, NULL, O_FIN}, {"urg", required_argument, NULL, O_URG},
+    {"ece", required_argument, NULL, O_ECE}, {"cwr", required_argument, NULL, O_CWR},
+    {"pmin", required_argument, NULL, O_PMIN}, {"pmax", required_argument, NULL, O_PMAX},
+    {"pstatic", required_argument, NULL, O_PSTATIC}, {"pexact", required_argument, NULL, O_PEXACT},
+    {"pfile", required_argument, NULL, O_PFILE}, {"pstring", required_argument, NULL, O_PSTRING},
+    {"time", required_argument, NULL, O_TIME}, {NULL, 0, NULL, 0},
+};
+
+/* defaults of one sequence (README.md:216-575; PB-Common clear_sequence) */
+static void clear_sequence(pb_config_t *c, int i)
+{
+    pb_sequence_t *s = &c->seq[i];
+    memset(s, 0, sizeof *s);
+    s->block = 1;
+    s->delay = 1000000;
+    s->l4_csum = 1;
+    s->ip.csum = 1;
+    s->ip.min_ttl = 64;
+    s->ip.max_ttl = 64;
+    s->ip.max_id = 64000;
+}
+
+/* first pass: common options and the -z overrides of sequence 0 */
+static void parse_common(int argc, char **argv, cmd_line_t *cmd, pb_sequence_t *s, const char **iface)
+{
+    int o;
+    while ((o = getopt_long(argc, argv, "c:lvhz", common_opts, NULL)) != -1)
+    {
+        const char *a = optarg;
+        switch (o)
+        {
+        case 'c': cmd->config = a; break;
+        case 'l': cmd->list = 1; break;
+        case 'v': cmd->verbose = 1; break;
+        case 'h': cmd->help = 1; break;
+        case 'z': cmd->cli = 1; break;
+        case O_INTERFACE: *iface = a; s->interface = a; break;
+        case O_BLOCK: s->block = (uint8_t)atoi(a); break;
+        case O_TRACK: s->track = (uint8_t)atoi(a); break;
+        case O_MAXPCKTS: s->max_pckts = strtoull(a, NULL, 10); break;
+        case O_MAXBYTES: s->max_bytes = strtoull(a, NULL, 10); break;
+        case O_PPS: s->pps = strtoull(a, NULL, 10); break;
+        case O_BPS: s->bps = strtoull(a, NULL, 10); break;
+        case O_DELAY: s->delay = strtoull(a, NULL, 10); break;
+        case O_THREADS: s->threads = (uint16_t)atoi(a); break;
+        case O_L4CSUM: s->l4_csum = (uint8_t)atoi(a); break;
+        case O_SMAC: s->eth.src_mac = a; break;
+        case O_DMAC: s->eth.dst_mac = a; break;
+        case O_MINTTL: s->ip.min_ttl = (uint8_t)atoi(a); break;
+        case O_MAXTTL: s->ip.max_ttl = (uint8_t)atoi(a); break;
+        case O_MINID: s->ip.min_id = (uint16_t)atoi(a); break;
+        case O_MAXID: s->ip.max_id = (uint16_t)atoi(a); break;
+        case O_SIP: /* "one range is supported in CIDR format" (README.md:132) */
+            if (strchr(a, '/'))
+            {
+                s->ip.ranges[0] = a;
+                s->ip.range_count = 1;
+                s->ip.src_ip = NULL;
+            }
+            else
+            {
+                s->ip.src_ip = a;
+            }
+            break;
+        case O_DIP: s->ip.dst_ip = a; break;
+        case O_PROTOCOL: s->ip.protocol = a; break;
+        case O_TOS: s->ip.tos = (uint8_t)atoi(a); break;
+        case O_L3CSUM: s->ip.csum = (uint8_t)atoi(a); break;
+        case O_USPORT: s->udp.src_port = (uint16_t)atoi(a); break;
+        case O_UDPORT: s->udp.dst_port = (uint16_t)atoi(a); break;
+        case O_TSPORT: s->tcp.src_port = (uint16_t)atoi(a); break;
+        case O_TDPORT: s->tcp.dst_port = (uint16_t)atoi(a); break;
+        case O_SYN: s->tcp.syn = (uint8_t)atoi(a); break;
+        case O_ACK: s->tcp.ack = (uint8_t)atoi(a); break;
+        case O_PSH: s->tcp.psh = (uint8_t)atoi(a); break;
+        case O_RST: s->tcp.rst = (uint8_t)atoi(a); break;
+        case O_FIN: s->tcp.fin = (uint8_t)atoi(a); break;
+        case O_URG: s->tcp.urg = (uint8_t)atoi(a); break;
+        case O_ECE: s->tcp.ece = (uint8_t)atoi(a); break;
+        case O_CWR: s->tcp.cwr = (uint8_t)atoi(a); break;
+        case O_PMIN: s->pls[0].min_len = (uint16_t)atoi(a); s->pl_cnt = 1; break;
+        case O_PMAX: s->pls[0].max_len = (uint16_t)atoi(a); s->pl_cnt = 1; break;
+        case O_PSTATIC: s->pls[0].is_static = (uint8_t)atoi(a); s->pl_cnt = 1; break;
+        case O_PEXACT: s->pls[0].exact = a; s->pl_cnt = 1; break;
+        case O_PFILE: s->pls[0].is_file = (uint8_t)atoi(a); s->pl_cnt = 1; break;
+        case O_PSTRING: s->pls[0].is_string = (uint8_t)atoi(a); s->pl_cnt = 1; break;
+        case O_TIME: s->time = strtoull(a, NULL, 10); break;
+        default: break;
+        }
+    }
+}
+
+static void print_cmd_help(void)
+{
+    fprintf(stdout, "Usage: pcktbatch-gpu -c <configfile> | -z [overrides] [-v -l -h] [AF_XDP/GPU options]\n\n"
+                    "-c --cfg => Path to the config file (JSON configs: use the Python loader).\n"
+                    "-l --list => Print basic information about sequences.\n"
+                    "-v --verbose => Provide verbose output.\n"
+                    "-h --help => Print out help menu and exit program.\n"
+                    "-z --cli => Enables the first sequence/packet override (README.md first-sequence options).\n\n"
+                    "AF_XDP: --queue --nowakeup --sharedumem --batchsize --skb --zerocopy --copy\n"
+                    "GPU: --gpus N --gpu I --gpubatch K --seed S --literal --singlefold --pcap FILE\n");
+}
+
+int main(int argc, char **argv)
+{
+    opterr = 0; /* main.c:26 */
+    cmd_line_t cmd = {0};
+    cfg = (pb_config_t *)calloc(1, sizeof *cfg);
+    if (cfg == NULL)
+        return EXIT_FAILURE;
+    for (int i = 0; i < PB_MAX_SEQUENCES; ++i)
+        clear_sequence(cfg, i);
+    const char *iface = NULL;
+    parse_common(argc, argv, &cmd, &cfg->seq[0], &iface);
+    if (cmd.help)
+    {
+        print_cmd_help();
+        return EXIT_SUCCESS;
+    }
+    struct cmd_line_af_xdp cmd_af_xdp = {0};
+    cmd_line_af_xdp_defaults(&cmd_af_xdp);
+    optind = 0; /* main.c:45 */
+    parse_cmd_line_af_xdp(&cmd_af_xdp, argc, argv);
+    pb_set_verbose(cmd.verbose);
+
+    int seq_cnt = 0;
+    if (cmd.cli)
+    {
+        fprintf(stdout, "Using command line...\n");
+        seq_cnt = 1;
+        cfg->interface = iface;
+    }
+    else
+    {
+        fprintf(stderr, "No -z/--cli sequence given (JSON config '%s' needs the Python loader: "
+                        "pb-af-xdp_amd/pbgpu.py Sequence.from_config).\n",
+                cmd.config ? cmd.config : "/etc/pcktbatch/conf.json");
+        return EXIT_FAILURE;
+    }
+    if (cmd.list)
+    {
+        for (int i = 0; i < seq_cnt; ++i)
+            fprintf(stdout, "Sequence #%d: %s -> %s proto %s, %u payload(s)\n", i + 1,
+                    cfg->seq[i].ip.src_ip ? cfg->seq[i].ip.src_ip
+                                          : (cfg->seq[i].ip.range_count ? cfg->seq[i].ip.ranges[0] : "127.0.0.1"),
+                    cfg->seq[i].ip.dst_ip ? cfg->seq[i].ip.dst_ip : "(none)",
+                    cfg->seq[i].ip.protocol ? cfg->seq[i].ip.protocol : "udp", cfg->seq[i].pl_cnt);
+        return EXIT_SUCCESS;
+    }
+    pb_pcap_t *pcap = NULL;
+    if (cmd_af_xdp.pcap)
+    {
+        pcap = pb_pcap_open(cmd_af_xdp.pcap);
+        if (pcap == NULL)
+        {
+            fprintf(stderr, "Cannot open pcap file %s.\n", cmd_af_xdp.pcap);
+            return EXIT_FAILURE;
+        }
+        pb_set_tx_hook(pb_pcap_tx, pcap);
+    }
+    signal(SIGINT, sign_hdl);
+    signal(SIGTERM, sign_hdl);
+    for (int i = 0; i < seq_cnt; ++i)
+        seq_send(cfg->interface, cfg->seq[i], (uint16_t)seq_cnt, cmd_af_xdp);
+    shutdown_prog(cfg, 0);
+    pb_pcap_close(pcap);
+    const int err = pb_last_error();
+    free(cfg);
+    return err ? EXIT_FAILURE : EXIT_SUCCESS;
+}

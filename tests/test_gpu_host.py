@@ -1,0 +1,61 @@
+"""The C host driver end to end on the GPU: pcktbatch-gpu -z (the reference's
+first-sequence CLI) builds frames through libpbgpu, lands them in UMEM slots
+and writes them to a pcap through the TX hook; the capture must equal the
+oracle's frames for the same sequence and seed stream."""
+import os
+import struct
+import subprocess
+
+import pytest
+
+import oracle_binding as ob
+import pb_configs as pc
+from pbgpu import Sequence
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "pb-af-xdp_amd", "bin", "pcktbatch-gpu")
+
+
+def read_pcap(path):
+    with open(path, "rb") as f:
+        data = f.read()
+    assert struct.unpack("<I", data[:4])[0] == 0xA1B2C3D4 and struct.unpack("<I", data[20:24])[0] == 1
+    frames, pos = [], 24
+    while pos < len(data):
+        _, _, incl, orig = struct.unpack("<IIII", data[pos:pos + 16])
+        frames.append(data[pos + 16:pos + 16 + incl])
+        pos += 16 + incl
+    return frames
+
+
+@pytest.mark.parametrize("batch", [2000, 4096])
+def test_cli_pcap_equals_oracle(tmp_path, batch):
+    pcap = tmp_path / "out.pcap"
+    seed = 0x1234567
+    cmd = [BIN, "-z", "--interface", "eth0", "--smac", pc.SMAC, "--dmac", pc.DMAC, "--dip", pc.DIP,
+           "--sip", "10.20.0.0/16", "--protocol", "udp", "--udport", "27015", "--pmin", "22", "--pmax", "22",
+           "--maxpckts", "5000", "--delay", "0", "--track", "1", "--gpubatch", str(batch), "--seed", str(seed),
+           "--pcap", str(pcap)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Completed 1 sequences!" in r.stdout and "total of 5000 packets" in r.stdout
+    got = read_pcap(pcap)
+    want = ob.frames(Sequence.from_config(pc.c2_udp_64()), 0, 0, 5000, seed)
+    assert len(got) == 5000
+    assert got == want
+
+
+def test_cli_variable_tcp_time_limited(tmp_path):
+    pcap = tmp_path / "tcp.pcap"
+    cmd = [BIN, "-z", "--interface", "eth0", "--dip", pc.DIP, "--sip", "172.16.0.0/12", "--protocol", "tcp",
+           "--tdport", "80", "--syn", "1", "--pmin", "0", "--pmax", "900", "--maxpckts", "3000", "--delay", "0",
+           "--gpubatch", "1000", "--seed", "7", "--pcap", str(pcap)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    got = read_pcap(pcap)
+    cfg = {"eth": {}, "ip": {"dip": pc.DIP, "ranges": ["172.16.0.0/12"], "protocol": "tcp"},
+           "tcp": {"dport": 80, "syn": 1}, "payloads": [{"length": {"min": 0, "max": 900}}]}
+    want = ob.frames(Sequence.from_config(cfg), 0, 0, 3000, 7)
+    assert got == want
