@@ -38,7 +38,7 @@ enum
     O_INTERFACE = 256, O_BLOCK, O_TRACK, O_MAXPCKTS, O_MAXBYTES, O_PPS, O_BPS, O_DELAY, O_THREADS, O_L4CSUM, O_SMAC,
     O_DMAC, O_MINTTL, O_MAXTTL, O_MINID, O_MAXID, O_SIP, O_DIP, O_PROTOCOL, O_TOS, O_L3CSUM, O_USPORT, O_UDPORT,
     O_TSPORT, O_TDPORT, O_SYN, O_ACK, O_PSH, O_RST, O_FIN, O_URG, O_ECE, O_CWR, O_PMIN, O_PMAX, O_PSTATIC, O_PEXACT,
-    O_PFILE, O_PSTRING, O_TIME,
+    O_PFILE, O_PSTRING, O_TIME, O_SECOND_PASS,
 };
 
 static const struct option common_opts[] = {
@@ -64,7 +64,17 @@ static const struct option common_opts[] = {
     {"pmin", required_argument, NULL, O_PMIN}, {"pmax", required_argument, NULL, O_PMAX},
     {"pstatic", required_argument, NULL, O_PSTATIC}, {"pexact", required_argument, NULL, O_PEXACT},
     {"pfile", required_argument, NULL, O_PFILE}, {"pstring", required_argument, NULL, O_PSTRING},
-    {"time", required_argument, NULL, O_TIME}, {NULL, 0, NULL, 0},
+    {"time", required_argument, NULL, O_TIME},
+    /* parsed in the second pass (cmd_line.c); listed here so that GNU getopt's
+     * argument permutation never separates them from their values */
+    {"queue", required_argument, NULL, O_SECOND_PASS}, {"batchsize", required_argument, NULL, O_SECOND_PASS},
+    {"nowakeup", no_argument, NULL, O_SECOND_PASS}, {"sharedumem", no_argument, NULL, O_SECOND_PASS},
+    {"skb", no_argument, NULL, O_SECOND_PASS}, {"zerocopy", no_argument, NULL, O_SECOND_PASS},
+    {"copy", no_argument, NULL, O_SECOND_PASS}, {"gpus", required_argument, NULL, O_SECOND_PASS},
+    {"gpu", required_argument, NULL, O_SECOND_PASS}, {"gpubatch", required_argument, NULL, O_SECOND_PASS},
+    {"seed", required_argument, NULL, O_SECOND_PASS}, {"literal", no_argument, NULL, O_SECOND_PASS},
+    {"singlefold", no_argument, NULL, O_SECOND_PASS}, {"pcap", required_argument, NULL, O_SECOND_PASS},
+    {NULL, 0, NULL, 0},
 };
 
 /* defaults of one sequence (README.md:216-575; PB-Common clear_sequence) */
@@ -201,6 +211,13 @@ int main(int argc, char **argv)
     }
     if (cmd.list)
     {
+        fprintf(stdout, "AF_XDP: queue_set=%u queue=%d nowakeup=%u sharedumem=%u batchsize=%u skb=%u zerocopy=%u copy=%u\n",
+                cmd_af_xdp.queue_set, cmd_af_xdp.queue, cmd_af_xdp.no_wake_up, cmd_af_xdp.shared_umem,
+                cmd_af_xdp.batch_size, cmd_af_xdp.skb_mode, cmd_af_xdp.zero_copy, cmd_af_xdp.copy);
+        fprintf(stdout, "GPU: gpus=%d gpu=%d gpubatch=%llu seed=%llu literal=%d singlefold=%d pcap=%s\n",
+                cmd_af_xdp.gpus, cmd_af_xdp.gpu_first, (unsigned long long)cmd_af_xdp.gpu_batch,
+                (unsigned long long)cmd_af_xdp.seed_base, cmd_af_xdp.literal_payload, cmd_af_xdp.single_fold,
+                cmd_af_xdp.pcap ? cmd_af_xdp.pcap : "(none)");
         for (int i = 0; i < seq_cnt; ++i)
             fprintf(stdout, "Sequence #%d: %s -> %s proto %s, %u payload(s)\n", i + 1,
                     cfg->seq[i].ip.src_ip ? cfg->seq[i].ip.src_ip

@@ -90,3 +90,15 @@ P(c.skb_mode = 1) P(c.zero_copy = 1) P(c.copy = 1) printf("%zu\n", sizeof c); }
     # this build's struct = the reference's 20 bytes + the GPU options
     assert int(lines[len(probe)]) == C.sizeof(cb.OurCmd) and C.sizeof(cb.RefCmd) == 20
     assert cb.OurCmd.gpus.offset == 20
+
+
+def test_two_pass_command_line():
+    """Common (-z) options and AF_XDP/GPU options interleaved in any order parse in
+    both passes (main.c:23-46 two-pass scheme) without getopt permutation losses."""
+    r = subprocess.run([BIN, "-z", "--seed", "77", "--interface", "eth0", "--queue", "3", "--sip", "10.20.0.0/16",
+                        "--pcap", "/tmp/x.pcap", "--dip", "10.0.0.2", "--gpubatch", "99", "--skb", "--protocol", "tcp",
+                        "--batchsize", "16", "--gpus", "2", "-l"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "queue_set=1 queue=3" in r.stdout and "batchsize=16 skb=1" in r.stdout
+    assert "gpus=2 gpu=0 gpubatch=99 seed=77" in r.stdout and "pcap=/tmp/x.pcap" in r.stdout
+    assert "10.20.0.0/16 -> 10.0.0.2 proto tcp" in r.stdout
