@@ -17,7 +17,11 @@
 #define PB_TILE_MAX (PB_WG * PB_CPL * 16)  // 16 KiB of output per workgroup
 #define PB_NF_MAX 260                      // frames touching one tile, max
 #define PB_IMG_DW 16                       // header image: 64 B per frame
+#define PB_IMG_STRIDE 20                   // dwords per frame image row in LDS (16 used + pad: conflict-free b128 rows)
 #define PB_JNEG 80                         // jump table starts at j = -80
+#define PB_STAGE_L48 72                    // lcg48 entries the staged kernel keeps in LDS (> 4 + 64)
+#define PB_STAGE_LDS(wgf) ((size_t)(wgf) * (16 + 7) * 4 + 4 + PB_STAGE_L48 * 8) // its LDS besides the stage
+#define PB_LCG48_N 4200                    // lcg48[m] = L^(48 m), m < 4200 (> 16-B chunks of a 64 KiB frame)
 
 // glibc LCG
 #define PB_LCG_A 1103515245u
@@ -93,8 +97,12 @@ struct pb_kargs
     uint32_t small_ndw;     // >0: small fixed frames, one lane per frame, NDW dwords per lane
     uint32_t gpf_g;         // >0: group-per-frame kernel with G lanes per frame
     uint32_t gpf_rmode;     // 1: all payloads random, 0: all static, 2: mixed
+    uint32_t gpf_fpw;       // frames per workgroup (multiple of 256 / gpf_g, <= 256)
+    uint32_t stage_win;     // >0: staged kernel, window of W workgroup bytes per stage fill (>= longest frame)
+    uint32_t stage_bytes;   // its LDS stage size (multiple of 16, >= W + longest frame + 32)
+    uint32_t stage_wgf;     // its frames per workgroup (<= 256)
+    unsigned long long *dbg; // PB_TIMING builds only: per-workgroup phase timestamps
     const uint2 *lcg48;     // lcg48[m] = L^(48 m): one 16-B chunk of payload = 48 LCG steps
-    uint32_t nt_stores;     // 1: non-temporal output stores
     uint32_t stail[32];     // small kernel, static payload: payload bytes at frame dwords p0.. (p0 = (hl-2)/4)
 };
 

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/pbgpu.h"
@@ -80,6 +81,8 @@ struct pbgpu_ctx
     hipStream_t stream = nullptr;
     uint2 *d_jump = nullptr;
     uint2 *d_lcg48 = nullptr;
+    unsigned long long *d_dbg = nullptr; // PBGPU_TIMING: per-workgroup phase stamps
+    uint64_t dbg_cap = 0;
     unsigned long long *d_counters = nullptr; // [PB_MAX_SEQUENCES][4]
     seq_slot seqs[PB_MAX_SEQUENCES];
     std::vector<timing_pair> pending;
@@ -319,14 +322,14 @@ int pbgpu_open(int device, pbgpu_ctx **out)
         return PBGPU_EIO;
     }
     std::vector<uint2> jt = make_jump_table();
-    std::vector<uint2> l48(65);
+    std::vector<uint2> l48(PB_LCG48_N);
     {
         const uint32_t a3 = PB_LCG_A * PB_LCG_A * PB_LCG_A, c3 = PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u);
         uint32_t A16 = 1, C16 = 0; // L^48 = (L^3)^16
         for (int i = 0; i < 16; ++i)
             C16 = a3 * C16 + c3, A16 = a3 * A16;
         uint32_t A = 1, C = 0;
-        for (int m = 0; m < 65; ++m)
+        for (int m = 0; m < PB_LCG48_N; ++m)
         {
             l48[m] = make_uint2(A, C);
             A = A16 * A;
@@ -364,6 +367,8 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipFree(ctx->d_jump);
     if (ctx->d_lcg48)
         (void)hipFree(ctx->d_lcg48);
+    if (ctx->d_dbg)
+        (void)hipFree(ctx->d_dbg);
     if (ctx->d_counters)
         (void)hipFree(ctx->d_counters);
     if (ctx->h_stage)
@@ -637,8 +642,6 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         }
     }
     {
-        const char *nt = getenv("PBGPU_NT"); // output stores non-temporal by default
-        K.nt_stores = (nt && !atoi(nt)) ? 0 : 1;
         const char *kern = getenv("PBGPU_KERNEL"); // "tile": force the tile kernel (comparison only)
         const bool tile = kern && !strcmp(kern, "tile");
         if (tile)
@@ -669,6 +672,81 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             if (ge && (atoi(ge) == 8 || atoi(ge) == 16 || atoi(ge) == 32 || atoi(ge) == 64))
                 K.gpf_g = (uint32_t)atoi(ge);
             K.gpf_rmode = n_random == (int)pls.size() ? 1 : (n_random == 0 ? 0 : 2);
+            const uint32_t ngw = PB_WG / K.gpf_g; // frames in flight per workgroup
+            uint32_t fpw = PB_WG;
+            const char *fe = getenv("PBGPU_FPW");
+            if (fe && atoi(fe) > 0)
+                fpw = (uint32_t)atoi(fe);
+            fpw = fpw < ngw ? ngw : (fpw > PB_WG ? PB_WG : fpw);
+            K.gpf_fpw = fpw / ngw * ngw;
+
+            // staged kernel (frames assembled in LDS, each window of the output written
+            // as one contiguous run).  Lanes per frame G: the smallest of the group
+            // sizes that waste the fewest lanes on a frame's payload chunks whose
+            // 256 / G frames in flight span at most 26 KiB.  Fixed-length windows hold
+            // k * 256 / G frames (~20 KiB); variable-length windows PBGPU_STAGE_KB
+            // (default 24) KiB.  Measured (profiles/r01/stage): 1500-B frames 5.1 TB/s
+            // at G = 16, 16 frames per window (group-per-frame: 4.1); 1024-B 5.2 at 16
+            // frames; 9000-B 5.2 at G = 64.
+            // variable-length frames stay on the group-per-frame kernel unless
+            // PBGPU_KERNEL=stage (configs[2]: 3.45 TB/s there, 2.75-3.2 staged)
+            const bool gpf_only = (kern && !strcmp(kern, "gpf")) || (!K.fixed_len && !(kern && !strcmp(kern, "stage")));
+            const uint32_t avg = (minf + maxf) / 2;
+            const uint32_t npc = (avg - K.hl) / 16 + 2;
+            double umax = 0;
+            for (uint32_t gg : {8u, 16u, 32u, 64u})
+                umax = std::max(umax, (double)npc / (gg * ((npc + gg - 1) / gg)));
+            uint32_t sg = 64;
+            for (uint32_t gg : {8u, 16u, 32u, 64u})
+                if ((double)npc / (gg * ((npc + gg - 1) / gg)) >= umax - 0.02 && (PB_WG / gg) * avg <= 26 * 1024)
+                {
+                    sg = gg;
+                    break;
+                }
+            if (!K.fixed_len)
+                sg = 16;
+            if (ge && (atoi(ge) == 8 || atoi(ge) == 16 || atoi(ge) == 32 || atoi(ge) == 64))
+                sg = (uint32_t)atoi(ge);
+            uint32_t wgf = K.fixed_len ? 64 : 128;
+            if (const char *e = getenv("PBGPU_WGF"))
+                wgf = atoi(e) > 0 && atoi(e) <= PB_WG ? (uint32_t)atoi(e) : wgf;
+            const char *ekb = getenv("PBGPU_STAGE_KB");
+            uint32_t win, sbytes;
+            if (K.fixed_len)
+            {
+                const uint32_t ngw2 = PB_WG / sg;
+                uint32_t fw = ngw2 * std::max(1u, (20u * 1024) / (ngw2 * maxf));
+                if (ekb && atoi(ekb) > 0)
+                    fw = std::max(1u, (uint32_t)atoi(ekb) * 1024 / maxf);
+                if (fe && atoi(fe) > 0)
+                    fw = (uint32_t)atoi(fe);
+                const uint32_t fit = (uint32_t)((64 * 1024 - 48 - PB_STAGE_LDS(std::max(wgf, fw))) / maxf);
+                fw = std::max(1u, std::min(fw, fit)); // the stage must fit 64 KiB of LDS
+                win = fw * maxf;
+                sbytes = (win + 30 + 15) / 16 * 16;
+            }
+            else
+            {
+                const uint32_t skb = ekb && atoi(ekb) > 0 ? (uint32_t)atoi(ekb) : 24;
+                sbytes = (skb * 1024 + 15) / 16 * 16;
+                if (sbytes < 2 * maxf + 48)
+                    sbytes = (2 * maxf + 48 + 15) / 16 * 16;
+                win = sbytes - maxf - 32;
+            }
+            if (K.fixed_len)
+            {
+                const uint32_t fw = win / maxf; // whole windows per workgroup
+                wgf = std::min<uint32_t>(PB_WG / fw * fw, fw * ((wgf + fw - 1) / fw));
+            }
+            else
+                wgf = std::min<uint32_t>(PB_WG, std::max(wgf, win / minf + 1));
+            if (!gpf_only && sbytes + PB_STAGE_LDS(wgf) <= 64 * 1024)
+            {
+                K.gpf_g = sg;
+                K.stage_win = win;
+                K.stage_wgf = wgf;
+                K.stage_bytes = sbytes;
+            }
         }
     }
     // tile: power of two, <= 16 KiB, <= (PB_NF_MAX - 2) frames of minimum length
@@ -774,6 +852,38 @@ static int timed_pair(pbgpu_ctx *ctx, timing_pair *p)
 }
 
 // One batch of the hot loop, sequence.c:433-602.
+// Diagnostic (PBGPU_TIMING with a -DPB_TIMING=1 build): mean phase durations of
+// the staged kernel's workgroups and the mean number of resident workgroups.
+static void report_phase_timing(pbgpu_ctx *ctx, uint64_t n_wg)
+{
+    std::vector<unsigned long long> h(n_wg * 8);
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+        hipMemcpy(h.data(), ctx->d_dbg, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    double ph[4] = {0, 0, 0, 0}, life = 0;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    uint64_t n = 0;
+    for (uint64_t w = 0; w < n_wg; ++w)
+    {
+        const unsigned long long *r = &h[w * 8];
+        if (!r[0] || !r[6])
+            continue;
+        ++n;
+        for (int i = 0; i < 4; ++i)
+            ph[i] += (double)r[i + 1];
+        life += (double)(r[6] - r[0]);
+        t0 = r[0] < t0 ? r[0] : t0;
+        t1 = r[6] > t1 ? r[6] : t1;
+    }
+    if (!n)
+        return;
+    fprintf(stderr,
+            "{\"pbgpu_timing\": {\"workgroups\": %llu, \"cycles_A\": %.0f, \"cycles_B_sum\": %.0f, \"cycles_C_sum\": %.0f, "
+            "\"cycles_S_sum\": %.0f, \"life_us\": %.3f, \"span_us\": %.3f, \"resident_wg\": %.1f}}\n",
+            (unsigned long long)n, ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, life / n / 100.0, (t1 - t0) / 100.0,
+            life / (double)(t1 - t0));
+}
+
 int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, pbgpu_frames *out)
 {
     if (ctx == NULL || out == NULL || seq_idx >= PB_MAX_SEQUENCES)
@@ -828,9 +938,26 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     int rc = timed_pair(ctx, &tp);
     if (rc)
         return rc;
+    const bool timing = K.stage_win && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
+    const uint64_t n_wg = K.stage_wgf ? (nf + K.stage_wgf - 1) / K.stage_wgf : 0;
+    if (timing)
+    {
+        if (ctx->dbg_cap < n_wg)
+        {
+            if (ctx->d_dbg)
+                (void)hipFree(ctx->d_dbg);
+            ctx->d_dbg = nullptr;
+            HIPCHK(hipMalloc((void **)&ctx->d_dbg, n_wg * 8 * sizeof(unsigned long long)));
+            ctx->dbg_cap = n_wg;
+        }
+        HIPCHK(hipMemsetAsync(ctx->d_dbg, 0, n_wg * 8 * sizeof(unsigned long long), ctx->stream));
+        K.dbg = ctx->d_dbg;
+    }
     HIPCHK(hipEventRecord(tp.a, ctx->stream));
     HIPCHK(pbk_launch_build(&K, (uint32_t)n_tiles, ctx->stream));
     HIPCHK(hipEventRecord(tp.b, ctx->stream));
+    if (timing)
+        report_phase_timing(ctx, n_wg);
     ctx->pending.push_back(tp);
     if (ctx->pending.size() >= 4096)
     {
@@ -1076,7 +1203,9 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
     if (!S.loaded)
         return PBGPU_ENOENT;
     const pb_kargs &K = S.K;
-    if (K.gpf_g)
+    if (K.stage_win)
+        snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
+    else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.small_ndw)
         snprintf(buf, n, "pb_small_kernel<%u, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false");

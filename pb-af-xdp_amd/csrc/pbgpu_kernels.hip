@@ -27,7 +27,6 @@
 // except two counter adds per launch.
 #include "pb_device.h"
 
-#define PB_IMG_STRIDE 20   // dwords per frame image row (16 used + pad: conflict-free b128 rows)
 #define PB_SCAN_ITEMS 8    // frames per thread in the length scan kernels
 
 typedef uint32_t pb_u32x4 __attribute__((ext_vector_type(4)));
@@ -129,6 +128,21 @@ __device__ __forceinline__ uint32_t pb_bytemask(int lo, int hi, int t)
     const uint32_t ge = a <= 0 ? 0xFFFFFFFFu : (a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a)));
     const uint32_t lt = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * b)));
     return ge & lt;
+}
+
+// 16-B output store.  The store kind is fixed at compile time (PB_NT): a
+// runtime choice between a non-temporal and a plain store gets merged into one
+// plain store by the compiler, dropping the non-temporal bit.
+#ifndef PB_NT
+#define PB_NT 0
+#endif
+__device__ __forceinline__ void pb_st16(uint8_t *p, pb_u32x4 v)
+{
+#if PB_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
+#else
+    *reinterpret_cast<pb_u32x4 *>(p) = v;
+#endif
 }
 
 // 4 payload bytes from 4 consecutive LCG states: byte = state[23:16]
@@ -643,10 +657,7 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
             for (int t = 0; t < 4; ++t)
                 v[t] &= pb_range_mask(0, (int)tile_bytes - (int)(16 * c + 4 * t));
         }
-        if (K.nt_stores)
-            __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(out + 16 * c));
-        else
-            *reinterpret_cast<pb_u32x4 *>(out + 16 * c) = v;
+        pb_st16(out + 16 * c, v);
     }
     if (blockIdx.x == 0 && tid == 0)
     {
@@ -671,15 +682,12 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
 
 // store bytes [max(0,-q0), min(16, flen-q0)) of a 16-B chunk at p (16-B aligned)
 __device__ __forceinline__ void pb_store_chunk(uint8_t *p, uint32_t o0, uint32_t o1, uint32_t o2, uint32_t o3, int q0,
-                                               int flen, uint32_t nt)
+                                               int flen)
 {
     const int a = -q0, b = flen - q0;
     if (a <= 0 && b >= 16)
     {
-        if (nt)
-            __builtin_nontemporal_store(pb_u32x4{o0, o1, o2, o3}, reinterpret_cast<pb_u32x4 *>(p));
-        else
-            *reinterpret_cast<pb_u32x4 *>(p) = pb_u32x4{o0, o1, o2, o3};
+        pb_st16(p, pb_u32x4{o0, o1, o2, o3});
         return;
     }
     const uint32_t o[4] = {o0, o1, o2, o3};
@@ -742,9 +750,10 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
 
     const uint32_t tid = threadIdx.x;
     const uint32_t flags = K.flags;
-    const uint64_t fwg = (uint64_t)blockIdx.x * PB_WG;
+    const uint32_t fpw = K.gpf_fpw; // frames per workgroup: a multiple of 256 / G, at most 256
+    const uint64_t fwg = (uint64_t)blockIdx.x * fpw;
     const uint64_t left = K.n_frames - fwg;
-    const uint32_t nfr = left < PB_WG ? (uint32_t)left : PB_WG;
+    const uint32_t nfr = left < fpw ? (uint32_t)left : fpw;
     const int hl = (int)K.hl;
 
     // ---------------- phase A: one lane per frame ----------------
@@ -797,17 +806,17 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
     __syncthreads();
 
     // ---------------- phase B: G lanes per frame ----------------
-    constexpr uint32_t NG = 64 / G; // frames in flight per wave
-    const uint32_t lane = tid & 63u, wave = tid >> 6;
-    const uint32_t g = lane / G, lg = lane % G;
+    // Round p gives the workgroup's 256 / G groups frames p * (256 / G) + group, so
+    // the four waves write one contiguous front through the workgroup's output.
+    constexpr uint32_t NGW = PB_WG / G; // frames in flight per workgroup
+    const uint32_t grp = tid / G, lg = tid % G;
     const uint2 Ml = K.lcg48[lg], MG = K.lcg48[G];
-    const uint32_t nt = K.nt_stores;
 
-    for (uint32_t p = 0; p < 64 / NG; ++p)
+    for (uint32_t p = 0; p < fpw / NGW; ++p)
     {
-        const uint32_t fr = wave * 64 + p * NG + g;
+        const uint32_t fr = p * NGW + grp;
         if (fr >= nfr)
-            continue;
+            break;
         const uint64_t base = ((uint64_t)s_bhi[fr] << 32) | s_blo[fr];
         const int flen = (int)s_flen[fr];
         const int s0 = (int)(base & 15u);
@@ -843,16 +852,13 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
                 pb_chunk_payload(K, rnd, x, src, j0, 0, 16, o0, o1, o2, o3);
                 if (rnd)
                     acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
-                if (nt)
-                    __builtin_nontemporal_store(pb_u32x4{o0, o1, o2, o3}, reinterpret_cast<pb_u32x4 *>(out + 16 * m));
-                else
-                    *reinterpret_cast<pb_u32x4 *>(out + 16 * m) = pb_u32x4{o0, o1, o2, o3};
+                pb_st16(out + 16 * m, pb_u32x4{o0, o1, o2, o3});
             }
             else if (j0 >= nvalid && j0 >= 0)
             {
                 // past the drawn bytes (literal rule): zeros up to the frame end
                 if (!(m + 1 == nch && cov_out))
-                    pb_store_chunk(out + 16 * m, 0u, 0u, 0u, 0u, q0, flen, nt);
+                    pb_store_chunk(out + 16 * m, 0u, 0u, 0u, 0u, q0, flen);
             }
             else
             {
@@ -933,10 +939,260 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
                 }
                 const bool special = q0 == -s0 && cov_in; // holds the previous frame's tail too: store whole
                 if (!(m + 1 == nch && cov_out))
-                    pb_store_chunk(out + 16 * m, o0, o1, o2, o3, special ? 0 : q0, special ? 16 : flen, nt);
+                    pb_store_chunk(out + 16 * m, o0, o1, o2, o3, special ? 0 : q0, special ? 16 : flen);
             }
         }
     }
+    if (K.fixed_len && blockIdx.x == 0 && tid == 0)
+    {
+        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
+        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+    }
+}
+
+// ---------------- staged: frames assembled in LDS, streamed out whole ----------------
+//
+// Workgroup = K.stage_wgf (<= 256) consecutive frames.  Phase A (one lane per
+// frame) computes each frame's seed, fields, header image with the IPv4 checksum,
+// payload length and LCG entry state (sequence.c:433-561, 596-602).  The frames
+// then pass through an LDS stage window by window: window w holds the frames that
+// start in bytes [w W, (w + 1) W) of the workgroup's output (K.stage_win = W), so
+// a window's packed bytes, aligned to the absolute 16-B grid, fit the stage.
+//   B  G lanes per frame: every 16-B chunk holding payload is generated whole
+//      (glibc LCG, sequence.c:552-555) into the stage, its payload words summed
+//      for the L4 checksum (sequence.c:569-594) and reduced over the group.  Bytes
+//      a chunk covers outside the payload lie in this frame's or the next frame's
+//      header, which C overwrites.
+//   C  one lane per (frame, header dword): the headers with their L4 checksums,
+//      byte-exact over the stage.
+//   S  the window streamed to HBM as one contiguous run of 16-B stores; only the
+//      two chunks shared with the neighbouring windows are byte-masked.
+#ifndef PB_TIMING
+#define PB_TIMING 0
+#endif
+// diagnostic builds (-DPB_TIMING=1): per-workgroup stamps, slots 0 and 6 in the
+// 100 MHz real-time clock, slots 1..4 in shader cycles (summed over windows)
+#define PB_STAMP(i)                                                                                   \
+    do                                                                                                \
+    {                                                                                                 \
+        if (PB_TIMING && tid == 0 && K.dbg)                                                           \
+            K.dbg[(uint64_t)blockIdx.x * 8 + (i)] =                                                   \
+                ((i) == 0 || (i) == 6) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define PB_LAP(i, t)                                                                                  \
+    do                                                                                                \
+    {                                                                                                 \
+        if (PB_TIMING && tid == 0 && K.dbg)                                                           \
+        {                                                                                             \
+            const unsigned long long now = __builtin_amdgcn_s_memtime();                              \
+            K.dbg[(uint64_t)blockIdx.x * 8 + (i)] += now - (t);                                       \
+            (t) = now;                                                                                \
+        }                                                                                             \
+    } while (0)
+
+template <int G, int RMODE>
+__global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    uint8_t *const stage = reinterpret_cast<uint8_t *>(s_dyn);
+    const uint32_t WF = K.stage_wgf; // frames per workgroup (<= 256)
+    uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_dyn + (K.stage_bytes >> 2)); // lcg48[0 .. PB_STAGE_L48)
+    uint32_t *const s_img = s_dyn + (K.stage_bytes >> 2) + 2 * PB_STAGE_L48; // header image, 16 dwords per frame
+    uint32_t *const s_r = s_img + WF * 16; // frame start, relative to the workgroup's 16-B chunk
+    uint32_t *const s_len = s_r + WF;
+    uint32_t *const s_hs = s_len + WF;     // L4 header + pseudo header (+ static payload) word sum
+    uint32_t *const s_z = s_hs + WF;       // LCG state at the frame's first 16-B chunk
+    uint32_t *const s_nv = s_z + WF;       // nvalid | random << 31
+    uint32_t *const s_src = s_nv + WF;     // blob offset (static payload)
+    uint32_t *const s_win = s_src + WF;    // s_win[w]: first frame of window w, [nwin] = nfr
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t flags = K.flags;
+    const int hl = (int)K.hl;
+    const uint32_t W = K.stage_win;
+    const uint64_t f0 = (uint64_t)blockIdx.x * WF;
+    const uint64_t left = K.n_frames - f0;
+    const uint32_t nfr = left < WF ? (uint32_t)left : WF;
+    const uint64_t W0 = K.fixed_len ? f0 * K.fixed_len : K.offsets[f0];
+    const uint64_t wbase = W0 & ~15ull;
+    unsigned long long tlap = 0;
+    PB_STAMP(0);
+    if (PB_TIMING && tid == 0)
+        tlap = __builtin_amdgcn_s_memtime();
+
+    // ---------------- A: one lane per frame ----------------
+    if (tid < PB_STAGE_L48)
+        s_l48[tid] = K.lcg48[tid];
+    uint32_t my_r = 0;
+    if (tid < nfr)
+    {
+        const uint64_t f = f0 + tid;
+        uint64_t base;
+        uint32_t flen;
+        if (K.fixed_len)
+        {
+            base = f * K.fixed_len;
+            flen = K.fixed_len;
+        }
+        else
+        {
+            base = K.offsets[f];
+            flen = (uint32_t)(K.offsets[f + 1] - base);
+        }
+        uint64_t k;
+        uint32_t pi;
+        pb_frame_index(K, f, k, pi);
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+        const uint32_t r0 = pb_rand_r(s);
+        const pb_frame_pl P = pb_payload(K, s, pi);
+        uint32_t d[16];
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d);
+        uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) + pb_halves(d[12]) +
+                      pb_halves(d[13]);
+        if (flags & PBK_PSEUDO)
+            hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
+        if (!P.random)
+            hs += P.ssum;
+        pb_u32x4 *row = reinterpret_cast<pb_u32x4 *>(s_img + tid * 16);
+        row[0] = pb_u32x4{d[0], d[1], d[2], d[3]};
+        row[1] = pb_u32x4{d[4], d[5], d[6], d[7]};
+        row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
+        row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
+        my_r = (uint32_t)(base - wbase);
+        // state at payload index j = -((r % 16) + hl): the first byte of the frame's first chunk
+        const uint2 jt = K.jump[PB_JNEG - ((my_r & 15u) + (uint32_t)hl)];
+        s_r[tid] = my_r;
+        s_len[tid] = flen;
+        s_hs[tid] = hs;
+        s_z[tid] = P.random ? jt.x * P.st0 + jt.y : 0u;
+        s_nv[tid] = P.nvalid | (P.random << 31);
+        s_src[tid] = P.blob_off;
+    }
+    __syncthreads();
+    // window starts: frame t opens windows (r_{t-1} / W, r_t / W]  (W >= the longest frame)
+    if (tid < nfr)
+    {
+        const uint32_t w = my_r / W;
+        const uint32_t wp = tid ? s_r[tid - 1] / W : 0u;
+        if (tid == 0)
+            s_win[0] = 0;
+        for (uint32_t v = wp + 1; v <= w; ++v)
+            s_win[v] = tid;
+        if (tid == nfr - 1)
+            s_win[w + 1] = nfr;
+    }
+    __syncthreads();
+    const uint32_t nwin = s_r[nfr - 1] / W + 1;
+    PB_LAP(1, tlap);
+
+    constexpr uint32_t NGW = PB_WG / G; // frames in flight per workgroup
+    const uint32_t grp = tid / G, lg = tid % G;
+    const uint2 MG = s_l48[G];
+    for (uint32_t w = 0; w < nwin; ++w)
+    {
+        const uint32_t sb = s_win[w], se = s_win[w + 1];
+        const uint32_t R0 = s_r[sb];                      // window bytes [R0, R1), workgroup-relative
+        const uint32_t R1 = s_r[se - 1] + s_len[se - 1];
+        const uint32_t sbase = R0 & ~15u;
+
+        // ---------------- B: G lanes per frame, payload chunks -> stage ----------------
+        for (uint32_t fr = sb + grp; fr < se; fr += NGW)
+        {
+            const uint32_t r = s_r[fr] - sbase;
+            const int flen = (int)s_len[fr];
+            const int s0 = (int)(r & 15u);
+            const uint32_t cf = r >> 4;                   // stage chunk of the frame's first byte
+            const uint32_t nch = (uint32_t)(s0 + flen + 15) >> 4;
+            const uint32_t ma = (uint32_t)(s0 + hl) >> 4; // first chunk holding payload (<= 4)
+            const uint32_t nv = s_nv[fr];
+            const bool rnd = RMODE == 2 ? (nv >> 31) != 0 : RMODE == 1;
+            const int nvalid = (int)(nv & 0x7FFFFFFFu);
+            const uint32_t src = s_src[fr];
+            uint32_t m = ma + lg;
+            uint32_t x = 0;
+            if (rnd)
+            {
+                const uint2 Mm = s_l48[m];
+                x = __umul24(s_z[fr], Mm.x) + Mm.y;
+            }
+            uint32_t acc = 0;
+            for (; m < nch; m += G)
+            {
+                const int j0 = (int)(16 * m) - s0 - hl; // payload index of the chunk's first byte
+                uint32_t o0, o1, o2, o3;
+                pb_chunk_payload(K, rnd, x, src, j0, 0, 16, o0, o1, o2, o3);
+                if (j0 < 0 || j0 + 16 > nvalid)
+                {
+                    // chunk bytes outside the drawn payload: zero (past nvalid, literal
+                    // rule) or header bytes of this / the next frame, rewritten by C
+                    const int lo = -j0, hi = nvalid - j0;
+                    o0 &= pb_range_mask(lo, hi);
+                    o1 &= pb_range_mask(lo - 4, hi - 4);
+                    o2 &= pb_range_mask(lo - 8, hi - 8);
+                    o3 &= pb_range_mask(lo - 12, hi - 12);
+                }
+                if (rnd)
+                    acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
+                reinterpret_cast<pb_u32x4 *>(stage)[cf + m] = pb_u32x4{o0, o1, o2, o3};
+                x = __umul24(x, MG.x) + MG.y;
+            }
+#pragma unroll
+            for (int sft = 1; sft < G; sft <<= 1)
+                acc += __shfl_xor(acc, sft, 64);
+            if ((flags & PBK_L4_CSUM) && lg == 0)
+            {
+                uint32_t pc = pb_fold(acc);
+                if (r & 1u) // chunk sums were taken in output alignment
+                    pc = pb_bswap16(pc);
+                const uint32_t c = (~pb_fold(pb_fold(s_hs[fr]) + pc)) & 0xFFFFu;
+                s_img[fr * 16 + K.csum_dw] |= K.csum_hi ? (c << 16) : c;
+            }
+        }
+        __syncthreads();
+        PB_LAP(2, tlap);
+
+        // ---------------- C: headers -> stage, one lane per (frame, dword) ----------------
+        for (uint32_t t = tid; t < (se - sb) * 16; t += PB_WG)
+        {
+            const uint32_t fr = sb + (t >> 4), u = t & 15u;
+            const uint32_t r = s_r[fr] - sbase;
+            const uint32_t sh = r & 3u;
+            const uint32_t end = sh + (uint32_t)hl; // bytes of the frame's dword row the header owns: [sh, end)
+            if (4 * u < end)
+            {
+                const uint32_t *img = s_img + fr * 16;
+                const uint32_t hi = img[u];
+                const uint32_t lo = u > 0 ? img[u - 1] : 0u;
+                const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
+                const uint32_t b0 = u == 0 ? sh : 0u;
+                const uint32_t b1 = end - 4 * u < 4 ? end - 4 * u : 4u;
+                const uint32_t wd = (r >> 2) + u;
+                if (b0 == 0 && b1 == 4)
+                    s_dyn[wd] = v;
+                else
+                    for (uint32_t bb = b0; bb < b1; ++bb)
+                        stage[4 * wd + bb] = (uint8_t)(v >> (8 * bb));
+            }
+        }
+        __syncthreads();
+        PB_LAP(3, tlap);
+
+        // ---------------- S: stage -> HBM, contiguous 16-B stores ----------------
+        const uint32_t lo_b = R0 - sbase, hi_b = R1 - sbase;
+        const uint32_t nst = (hi_b + 15u) >> 4;
+        uint8_t *const gout = K.out + wbase + sbase;
+        for (uint32_t c = tid; c < nst; c += PB_WG)
+        {
+            const pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(stage)[c];
+            if ((c == 0 && lo_b) || 16 * c + 16 > hi_b)
+                pb_store_chunk(gout + 16 * c, v[0], v[1], v[2], v[3], (int)(16 * c) - (int)lo_b, (int)(hi_b - lo_b));
+            else
+                pb_st16(gout + 16 * c, v);
+        }
+        __syncthreads(); // the next window reuses the stage
+        PB_LAP(4, tlap);
+    }
+    PB_STAMP(6);
     if (K.fixed_len && blockIdx.x == 0 && tid == 0)
     {
         atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
@@ -1110,9 +1366,9 @@ static void pbk_launch_small(const pb_kargs *K, uint32_t grid, hipStream_t st)
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid, hipStream_t st)
 {
-    if (K->gpf_g)
+    if (K->gpf_g && !K->stage_win)
     {
-        const uint32_t grid = (uint32_t)((K->n_frames + PB_WG - 1) / PB_WG);
+        const uint32_t grid = (uint32_t)((K->n_frames + K->gpf_fpw - 1) / K->gpf_fpw);
         const uint32_t rm = K->gpf_rmode;
 #define PB_GPF(GG, RM) hipLaunchKernelGGL((pb_gpf_kernel<GG, RM>), dim3(grid), dim3(PB_WG), 0, st, *K)
 #define PB_GPF_RM(GG)      \
@@ -1140,6 +1396,38 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid,
         }
 #undef PB_GPF_RM
 #undef PB_GPF
+    }
+    else if (K->stage_win)
+    {
+        const uint32_t grid = (uint32_t)((K->n_frames + K->stage_wgf - 1) / K->stage_wgf);
+        const size_t lds = K->stage_bytes + PB_STAGE_LDS(K->stage_wgf);
+        const uint32_t rm = K->gpf_rmode;
+#define PB_STG(GG, RM) hipLaunchKernelGGL((pb_stage_kernel<GG, RM>), dim3(grid), dim3(PB_WG), lds, st, *K)
+#define PB_STG_RM(GG)      \
+    if (rm == 1)           \
+        PB_STG(GG, 1);     \
+    else if (rm == 0)      \
+        PB_STG(GG, 0);     \
+    else                   \
+        PB_STG(GG, 2)
+        if (K->gpf_g == 8)
+        {
+            PB_STG_RM(8);
+        }
+        else if (K->gpf_g == 16)
+        {
+            PB_STG_RM(16);
+        }
+        else if (K->gpf_g == 32)
+        {
+            PB_STG_RM(32);
+        }
+        else
+        {
+            PB_STG_RM(64);
+        }
+#undef PB_STG_RM
+#undef PB_STG
     }
     else if (K->small_ndw)
     {

@@ -1,0 +1,88 @@
+"""GPU parity of every kernel shape the library can select, not only the
+default one: the staged kernel at other lane-group / window / workgroup sizes,
+the group-per-frame kernel (the fallback for frames too long for an LDS stage)
+and the tile kernel, each bit-exact against the CPU oracle on every config.
+Selection is through the library's PBGPU_* environment overrides, which
+pbgpu_load_sequence() reads.  Run on the MI355X box: pytest -m gpu."""
+import copy
+
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+import pb_configs as pc
+from pbgpu import GpuContext, Sequence
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [
+    ("gpf", {"PBGPU_KERNEL": "gpf"}, ("pb_gpf_kernel", "pb_small_kernel")),
+    ("tile", {"PBGPU_KERNEL": "tile"}, ("pb_build_kernel",)),
+    ("stage_g8_wgf5", {"PBGPU_KERNEL": "stage", "PBGPU_G": "8", "PBGPU_WGF": "5"},
+     ("pb_stage_kernel<8", "pb_small_kernel")),
+    ("stage_g64_kb4", {"PBGPU_KERNEL": "stage", "PBGPU_G": "64", "PBGPU_STAGE_KB": "4"},
+     ("pb_stage_kernel<64", "pb_small_kernel")),
+    ("stage_g32_kb36", {"PBGPU_KERNEL": "stage", "PBGPU_G": "32", "PBGPU_STAGE_KB": "36"},
+     ("pb_stage_kernel<32", "pb_small_kernel")),
+]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = GpuContext(0)
+    yield c
+    c.close()
+
+
+def _iters(cfg, budget=6 << 20):
+    mx = 54 + max([p.get("length", {}).get("max", 0) for p in cfg.get("payloads", [])] + [256])
+    return max(32, min(6000, budget // mx))
+
+
+def _check(ctx, cfg, first, n, rule=0, fold=0):
+    seq = Sequence.from_config(cfg)
+    ctx.load_sequence(5, seq, pc.SEED_BASE, payload_rule=rule, iph_fold=fold)
+    fb = ctx.alloc_frames(*ctx.build_size(5, n))
+    ctx.build(5, first, n, fb)
+    ctx.sync()
+    g_data, g_off = fb.packed(), fb.offsets()
+    fb.free()
+    o_data, o_off = ob.build(seq, 5, first, n, pc.SEED_BASE, payload_rule=rule, iph_fold=fold)
+    assert np.array_equal(g_off, o_off)
+    if not np.array_equal(g_data, o_data):
+        bad = int(np.nonzero(g_data != o_data)[0][0])
+        f = int(np.searchsorted(o_off, bad, side="right") - 1)
+        pytest.fail(f"first mismatch at byte {bad} (frame {f}, offset {bad - int(o_off[f])})")
+    return ctx.kernel_name(5)
+
+
+@pytest.mark.parametrize("shape,env,kernels", SHAPES, ids=[s[0] for s in SHAPES])
+@pytest.mark.parametrize("name", pc.ALL)
+def test_kernel_shape_matches_oracle(ctx, monkeypatch, shape, env, kernels, name):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cfg = pc.get(name)
+    kern = _check(ctx, cfg, 123456789, _iters(cfg))
+    assert kern.startswith(kernels), kern
+
+
+@pytest.mark.parametrize("shape,env,kernels", SHAPES[:1] + SHAPES[2:3], ids=["gpf", "stage_g8_wgf5"])
+@pytest.mark.parametrize("name,rule,fold", pc.RULE_CASES)
+def test_kernel_shape_rules(ctx, monkeypatch, shape, env, kernels, name, rule, fold):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cfg = pc.get(name)
+    _check(ctx, cfg, 42, _iters(cfg), rule, fold)
+
+
+@pytest.mark.parametrize("plen", [57000, 60000, 65000])
+def test_huge_frames(ctx, plen):
+    """The longest frames: up to ~57 KB still fit the LDS stage; longer ones fall
+    back to the group-per-frame kernel.  Bit-exact either way."""
+    cfg = copy.deepcopy(pc.get("c2_udp_1500"))
+    cfg["payloads"] = [{"length": {"min": plen, "max": plen}}]
+    kern = _check(ctx, cfg, 7, 96)
+    assert kern.startswith("pb_stage_kernel" if plen < 58000 else "pb_gpf_kernel"), kern
+    cfg["payloads"] = [{"length": {"min": 30000, "max": plen}}]
+    kern = _check(ctx, cfg, 7, 96)
+    assert kern.startswith("pb_gpf_kernel"), kern
