@@ -100,7 +100,8 @@ struct pb_kargs
     uint32_t gpf_fpw;       // frames per workgroup (multiple of 256 / gpf_g, <= 256)
     uint32_t stage_win;     // >0: staged kernel, window of W workgroup bytes per stage fill (>= longest frame)
     uint32_t stage_bytes;   // its LDS stage size (multiple of 16, >= W + longest frame + 32)
-    uint32_t stage_wgf;     // its frames per workgroup (<= 256)
+    uint32_t stage_wgf;     // its frames per workgroup (<= its threads per workgroup)
+    uint32_t stage_wgt;     // its threads per workgroup: 256, or 64 (one wave, barriers are wave-local)
     unsigned long long *dbg; // PB_TIMING builds only: per-workgroup phase timestamps
     const uint2 *lcg48;     // lcg48[m] = L^(48 m): one 16-B chunk of payload = 48 LCG steps
     uint32_t stail[32];     // small kernel, static payload: payload bytes at frame dwords p0.. (p0 = (hl-2)/4)

@@ -259,7 +259,12 @@ int upload(T **dptr, const T *src, size_t n)
         (void)hipFree(*dptr);
     *dptr = nullptr;
     if (n == 0)
+    {
+        // an empty table is a zeroed 256-B allocation, never a null device pointer
+        HIPCHK(hipMalloc((void **)dptr, 256));
+        HIPCHK(hipMemset(*dptr, 0, 256));
         return PBGPU_OK;
+    }
     HIPCHK(hipMalloc((void **)dptr, n * sizeof(T)));
     HIPCHK(hipMemcpy(*dptr, src, n * sizeof(T), hipMemcpyHostToDevice));
     return PBGPU_OK;
@@ -707,15 +712,19 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 sg = 16;
             if (ge && (atoi(ge) == 8 || atoi(ge) == 16 || atoi(ge) == 32 || atoi(ge) == 64))
                 sg = (uint32_t)atoi(ge);
+            uint32_t wgt = PB_WG;
+            if (const char *e = getenv("PBGPU_WGT"))
+                wgt = atoi(e) == 64 ? 64 : PB_WG;
             uint32_t wgf = K.fixed_len ? 64 : 128;
             if (const char *e = getenv("PBGPU_WGF"))
                 wgf = atoi(e) > 0 && atoi(e) <= PB_WG ? (uint32_t)atoi(e) : wgf;
+            wgf = std::min(wgf, wgt);
             const char *ekb = getenv("PBGPU_STAGE_KB");
             uint32_t win, sbytes;
             if (K.fixed_len)
             {
-                const uint32_t ngw2 = PB_WG / sg;
-                uint32_t fw = ngw2 * std::max(1u, (20u * 1024) / (ngw2 * maxf));
+                const uint32_t ngw2 = std::max(1u, wgt / sg);
+                uint32_t fw = ngw2 * std::max(1u, (20u * 1024 * wgt / PB_WG) / (ngw2 * maxf));
                 if (ekb && atoi(ekb) > 0)
                     fw = std::max(1u, (uint32_t)atoi(ekb) * 1024 / maxf);
                 if (fe && atoi(fe) > 0)
@@ -736,15 +745,16 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             if (K.fixed_len)
             {
                 const uint32_t fw = win / maxf; // whole windows per workgroup
-                wgf = std::min<uint32_t>(PB_WG / fw * fw, fw * ((wgf + fw - 1) / fw));
+                wgf = fw > wgt ? wgt : std::min<uint32_t>(wgt / fw * fw, fw * ((wgf + fw - 1) / fw));
             }
             else
-                wgf = std::min<uint32_t>(PB_WG, std::max(wgf, win / minf + 1));
+                wgf = std::min<uint32_t>(wgt, std::max(wgf, win / minf + 1));
             if (!gpf_only && sbytes + PB_STAGE_LDS(wgf) <= 64 * 1024)
             {
                 K.gpf_g = sg;
                 K.stage_win = win;
                 K.stage_wgf = wgf;
+                K.stage_wgt = wgt;
                 K.stage_bytes = sbytes;
             }
         }

@@ -174,7 +174,20 @@ __device__ __forceinline__ uint32_t pb_window(const uint32_t *img, int x)
 // per-iteration fields + tot_len / udp len + IPv4 checksum, sequence.c:596-602),
 // frame bytes 0..63 as little-endian dwords; the L4 checksum field stays 0.
 // Returns the L4 length (header + payload).
-__device__ __forceinline__ uint32_t pb_header(const pb_kargs &K, uint32_t r0, uint32_t plen, uint32_t (&d)[16])
+// The source range of an iteration (sequence.c:455-497): one range is a uniform
+// (scalar) load that does not wait for the seed.
+// (No table unless the source is random: K.ranges may be null.)
+__device__ __forceinline__ uint2 pb_range(const pb_kargs &K, uint32_t r0)
+{
+    if (!(K.flags & PBK_RND_SADDR))
+        return make_uint2(0u, 0u);
+    if (K.rng.d == 1)
+        return K.ranges[0];
+    return K.ranges[pb_mod(r0, K.rng)];
+}
+
+__device__ __forceinline__ uint32_t pb_header(const pb_kargs &K, uint32_t r0, uint32_t plen, uint32_t (&d)[16],
+                                              uint2 rg)
 {
     const uint32_t flags = K.flags;
 #pragma unroll
@@ -186,7 +199,6 @@ __device__ __forceinline__ uint32_t pb_header(const pb_kargs &K, uint32_t r0, ui
         d[4] |= pb_bswap16((K.id_min + pb_mod(r0, K.id)) & 0xFFFFu) << 16;
     if (flags & PBK_RND_SADDR) // sequence.c:455-497
     {
-        const uint2 rg = K.ranges[K.rng.d == 1 ? 0u : pb_mod(r0, K.rng)];
         const uint32_t sa = __builtin_bswap32(rg.x | (r0 & rg.y));
         d[6] |= sa << 16;
         d[7] |= sa >> 16;
@@ -293,7 +305,7 @@ __global__ __launch_bounds__(PB_WG) void pb_build_kernel(pb_kargs K)
         const pb_frame_pl P = pb_payload(K, s, pi);
 
         uint32_t d[16];
-        const uint32_t l4tot = pb_header(K, r0, P.plen, d);
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d, pb_range(K, r0));
 
         // L4 header words (check field still 0) + pseudo header
         uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) +
@@ -533,7 +545,7 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
         const uint32_t r0 = pb_rand_r(s);
         const uint32_t plen = flen - HL;
         uint32_t h[16];
-        const uint32_t l4tot = pb_header(K, r0, plen, h);
+        const uint32_t l4tot = pb_header(K, r0, plen, h, pb_range(K, r0));
         uint32_t d[NDW];
 #pragma unroll
         for (int t = 0; t < NDW; ++t)
@@ -779,7 +791,7 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
         const uint32_t r0 = pb_rand_r(s);
         const pb_frame_pl P = pb_payload(K, s, pi);
         uint32_t d[16];
-        const uint32_t l4tot = pb_header(K, r0, P.plen, d);
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d, pb_range(K, r0));
         uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) + pb_halves(d[12]) +
                       pb_halves(d[13]);
         if (flags & PBK_PSEUDO)
@@ -952,7 +964,8 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
 
 // ---------------- staged: frames assembled in LDS, streamed out whole ----------------
 //
-// Workgroup = K.stage_wgf (<= 256) consecutive frames.  Phase A (one lane per
+// Workgroup = K.stage_wgf consecutive frames (at most WGT: 256 threads, or 64,
+// one wave, whose barriers cost nothing).  Phase A (one lane per
 // frame) computes each frame's seed, fields, header image with the IPv4 checksum,
 // payload length and LCG entry state (sequence.c:433-561, 596-602).  The frames
 // then pass through an LDS stage window by window: window w holds the frames that
@@ -990,8 +1003,30 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
         }                                                                                             \
     } while (0)
 
-template <int G, int RMODE>
-__global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
+// Sum over aligned groups of G lanes (G = 8, 16, 32, 64), result in every lane
+// of the group: in-row steps by DPP (no LDS round trip), the rest by swizzle /
+// shuffle.
+template <int G>
+__device__ __forceinline__ uint32_t pb_group_sum(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false); // quad_perm [2,3,0,1]
+    if (G == 8)
+        v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F); // xor 4
+    if (G >= 16)
+    {
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false); // row_ror:4
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false); // row_ror:8
+    }
+    if (G >= 32)
+        v += __shfl_xor(v, 16, 64);
+    if (G >= 64)
+        v += __shfl_xor(v, 32, 64);
+    return v;
+}
+
+template <int G, int RMODE, int WGT>
+__global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     uint8_t *const stage = reinterpret_cast<uint8_t *>(s_dyn);
@@ -1021,8 +1056,12 @@ __global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
         tlap = __builtin_amdgcn_s_memtime();
 
     // ---------------- A: one lane per frame ----------------
-    if (tid < PB_STAGE_L48)
-        s_l48[tid] = K.lcg48[tid];
+    // the table loads are issued first; their latency hides behind the seed arithmetic
+    uint2 l48v[(PB_STAGE_L48 + WGT - 1) / WGT];
+#pragma unroll
+    for (uint32_t i = 0; i < (PB_STAGE_L48 + WGT - 1) / WGT; ++i)
+        if (tid + i * WGT < PB_STAGE_L48)
+            l48v[i] = K.lcg48[tid + i * WGT];
     uint32_t my_r = 0;
     if (tid < nfr)
     {
@@ -1039,6 +1078,10 @@ __global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
             base = K.offsets[f];
             flen = (uint32_t)(K.offsets[f + 1] - base);
         }
+        my_r = (uint32_t)(base - wbase);
+        // state at payload index j = -((r % 16) + hl): the first byte of the frame's first chunk
+        const uint2 jt = K.jump[PB_JNEG - ((my_r & 15u) + (uint32_t)hl)];
+        const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
         uint64_t k;
         uint32_t pi;
         pb_frame_index(K, f, k, pi);
@@ -1046,7 +1089,7 @@ __global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
         const uint32_t r0 = pb_rand_r(s);
         const pb_frame_pl P = pb_payload(K, s, pi);
         uint32_t d[16];
-        const uint32_t l4tot = pb_header(K, r0, P.plen, d);
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
         uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) + pb_halves(d[12]) +
                       pb_halves(d[13]);
         if (flags & PBK_PSEUDO)
@@ -1058,9 +1101,6 @@ __global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
         row[1] = pb_u32x4{d[4], d[5], d[6], d[7]};
         row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
         row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
-        my_r = (uint32_t)(base - wbase);
-        // state at payload index j = -((r % 16) + hl): the first byte of the frame's first chunk
-        const uint2 jt = K.jump[PB_JNEG - ((my_r & 15u) + (uint32_t)hl)];
         s_r[tid] = my_r;
         s_len[tid] = flen;
         s_hs[tid] = hs;
@@ -1068,6 +1108,10 @@ __global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
         s_nv[tid] = P.nvalid | (P.random << 31);
         s_src[tid] = P.blob_off;
     }
+#pragma unroll
+    for (uint32_t i = 0; i < (PB_STAGE_L48 + WGT - 1) / WGT; ++i)
+        if (tid + i * WGT < PB_STAGE_L48)
+            s_l48[tid + i * WGT] = l48v[i];
     __syncthreads();
     // window starts: frame t opens windows (r_{t-1} / W, r_t / W]  (W >= the longest frame)
     if (tid < nfr)
@@ -1085,7 +1129,7 @@ __global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
     const uint32_t nwin = s_r[nfr - 1] / W + 1;
     PB_LAP(1, tlap);
 
-    constexpr uint32_t NGW = PB_WG / G; // frames in flight per workgroup
+    constexpr uint32_t NGW = WGT / G; // frames in flight per workgroup
     const uint32_t grp = tid / G, lg = tid % G;
     const uint2 MG = s_l48[G];
     for (uint32_t w = 0; w < nwin; ++w)
@@ -1136,9 +1180,7 @@ __global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
                 reinterpret_cast<pb_u32x4 *>(stage)[cf + m] = pb_u32x4{o0, o1, o2, o3};
                 x = __umul24(x, MG.x) + MG.y;
             }
-#pragma unroll
-            for (int sft = 1; sft < G; sft <<= 1)
-                acc += __shfl_xor(acc, sft, 64);
+            acc = pb_group_sum<G>(acc);
             if ((flags & PBK_L4_CSUM) && lg == 0)
             {
                 uint32_t pc = pb_fold(acc);
@@ -1152,7 +1194,7 @@ __global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
         PB_LAP(2, tlap);
 
         // ---------------- C: headers -> stage, one lane per (frame, dword) ----------------
-        for (uint32_t t = tid; t < (se - sb) * 16; t += PB_WG)
+        for (uint32_t t = tid; t < (se - sb) * 16; t += WGT)
         {
             const uint32_t fr = sb + (t >> 4), u = t & 15u;
             const uint32_t r = s_r[fr] - sbase;
@@ -1178,16 +1220,31 @@ __global__ __launch_bounds__(PB_WG) void pb_stage_kernel(pb_kargs K)
         PB_LAP(3, tlap);
 
         // ---------------- S: stage -> HBM, contiguous 16-B stores ----------------
+        // whole chunks [c0, c1) two per lane per step (both LDS reads in flight
+        // before the stores); the chunks shared with the neighbouring windows,
+        // 0 and c1, are byte-masked (a window is >= 42 B, so they differ)
         const uint32_t lo_b = R0 - sbase, hi_b = R1 - sbase;
-        const uint32_t nst = (hi_b + 15u) >> 4;
+        const uint32_t c0 = lo_b ? 1u : 0u, c1 = hi_b >> 4;
         uint8_t *const gout = K.out + wbase + sbase;
-        for (uint32_t c = tid; c < nst; c += PB_WG)
+        const pb_u32x4 *const st16 = reinterpret_cast<const pb_u32x4 *>(stage);
+        for (uint32_t c = c0 + tid; c < c1; c += 2 * WGT)
         {
-            const pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(stage)[c];
-            if ((c == 0 && lo_b) || 16 * c + 16 > hi_b)
-                pb_store_chunk(gout + 16 * c, v[0], v[1], v[2], v[3], (int)(16 * c) - (int)lo_b, (int)(hi_b - lo_b));
-            else
-                pb_st16(gout + 16 * c, v);
+            const bool two = c + WGT < c1;
+            const pb_u32x4 v0 = st16[c];
+            const pb_u32x4 v1 = two ? st16[c + WGT] : v0;
+            pb_st16(gout + 16 * c, v0);
+            if (two)
+                pb_st16(gout + 16 * (c + WGT), v1);
+        }
+        if (tid == 0 && lo_b)
+        {
+            const pb_u32x4 v = st16[0];
+            pb_store_chunk(gout, v[0], v[1], v[2], v[3], -(int)lo_b, (int)(hi_b - lo_b));
+        }
+        if (tid == WGT - 1 && (hi_b & 15u))
+        {
+            const pb_u32x4 v = st16[c1];
+            pb_store_chunk(gout + 16 * c1, v[0], v[1], v[2], v[3], (int)(16 * c1) - (int)lo_b, (int)(hi_b - lo_b));
         }
         __syncthreads(); // the next window reuses the stage
         PB_LAP(4, tlap);
@@ -1402,7 +1459,14 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid,
         const uint32_t grid = (uint32_t)((K->n_frames + K->stage_wgf - 1) / K->stage_wgf);
         const size_t lds = K->stage_bytes + PB_STAGE_LDS(K->stage_wgf);
         const uint32_t rm = K->gpf_rmode;
-#define PB_STG(GG, RM) hipLaunchKernelGGL((pb_stage_kernel<GG, RM>), dim3(grid), dim3(PB_WG), lds, st, *K)
+#define PB_STG(GG, RM)                                                                                     \
+    do                                                                                                     \
+    {                                                                                                      \
+        if (K->stage_wgt == 64)                                                                            \
+            hipLaunchKernelGGL((pb_stage_kernel<GG, RM, 64>), dim3(grid), dim3(64), lds, st, *K);          \
+        else                                                                                               \
+            hipLaunchKernelGGL((pb_stage_kernel<GG, RM, PB_WG>), dim3(grid), dim3(PB_WG), lds, st, *K);    \
+    } while (0)
 #define PB_STG_RM(GG)      \
     if (rm == 1)           \
         PB_STG(GG, 1);     \

@@ -22,6 +22,8 @@ SHAPES = [
      ("pb_stage_kernel<8", "pb_small_kernel")),
     ("stage_g64_kb4", {"PBGPU_KERNEL": "stage", "PBGPU_G": "64", "PBGPU_STAGE_KB": "4"},
      ("pb_stage_kernel<64", "pb_small_kernel")),
+    ("stage_wave", {"PBGPU_KERNEL": "stage", "PBGPU_WGT": "64", "PBGPU_WGF": "24"},
+     ("pb_stage_kernel", "pb_small_kernel")),
     ("stage_g32_kb36", {"PBGPU_KERNEL": "stage", "PBGPU_G": "32", "PBGPU_STAGE_KB": "36"},
      ("pb_stage_kernel<32", "pb_small_kernel")),
 ]
