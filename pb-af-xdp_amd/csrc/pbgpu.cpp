@@ -88,6 +88,9 @@ struct pbgpu_ctx
     std::vector<timing_pair> pending;
     std::vector<timing_pair> pool;
     uint8_t *h_stage = nullptr;
+    uint16_t *d_lens = nullptr; // copy_to_umem: frame lengths of the mapped scatter (device)
+    uint16_t *h_lens = nullptr; // ... and their pinned host copy
+    uint32_t lens_cap = 0;
     size_t h_stage_bytes = 0;
 };
 
@@ -378,6 +381,10 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipFree(ctx->d_counters);
     if (ctx->h_stage)
         (void)hipHostFree(ctx->h_stage);
+    if (ctx->d_lens)
+        (void)hipFree(ctx->d_lens);
+    if (ctx->h_lens)
+        (void)hipHostFree(ctx->h_lens);
     if (ctx->stream)
         (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1082,13 +1089,29 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
     uint16_t *d_lens = NULL;
     if (hipHostGetDevicePointer(&dev_dst, dst, 0) == hipSuccess && dev_dst != NULL)
     {
-        HIPCHK(hipMallocAsync((void **)&d_lens, (size_t)n * 2, ctx->stream));
+        // lengths go through buffers owned by the context (device + pinned host),
+        // never through a stream-ordered allocation or a pageable async copy
+        if (ctx->lens_cap < n)
+        {
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+            if (ctx->d_lens)
+                (void)hipFree(ctx->d_lens);
+            if (ctx->h_lens)
+                (void)hipHostFree(ctx->h_lens);
+            ctx->d_lens = NULL;
+            ctx->h_lens = NULL;
+            ctx->lens_cap = 0;
+            HIPCHK(hipMalloc((void **)&ctx->d_lens, (size_t)n * 2));
+            HIPCHK(hipHostMalloc((void **)&ctx->h_lens, (size_t)n * 2, 0));
+            ctx->lens_cap = n;
+        }
+        d_lens = ctx->d_lens;
         HIPCHK(pbk_launch_scatter(f->data, f->offsets, first_frame, n, (uint8_t *)dev_dst, slot_stride, d_lens,
                                   ctx->stream));
-        if (lens_out)
-            HIPCHK(hipMemcpyAsync(lens_out, d_lens, (size_t)n * 2, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(hipFreeAsync(d_lens, ctx->stream));
+        HIPCHK(hipMemcpyAsync(ctx->h_lens, d_lens, (size_t)n * 2, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));
+        if (lens_out)
+            memcpy(lens_out, ctx->h_lens, (size_t)n * 2);
         return PBGPU_OK;
     }
     (void)hipGetLastError();

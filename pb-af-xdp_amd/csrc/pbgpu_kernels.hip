@@ -692,6 +692,28 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
 // checksum.  Chunks shared with a neighbouring frame are written byte/dword-
 // masked, so every byte of the packed stream is written exactly once.
 
+// Sum over aligned groups of G lanes (G = 8, 16, 32, 64), result in every lane
+// of the group: in-row steps by DPP (no LDS round trip), the rest by swizzle /
+// shuffle.
+template <int G>
+__device__ __forceinline__ uint32_t pb_group_sum(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false); // quad_perm [2,3,0,1]
+    if (G == 8)
+        v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F); // xor 4
+    if (G >= 16)
+    {
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false); // row_ror:4
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false); // row_ror:8
+    }
+    if (G >= 32)
+        v += __shfl_xor(v, 16, 64);
+    if (G >= 64)
+        v += __shfl_xor(v, 32, 64);
+    return v;
+}
+
 // store bytes [max(0,-q0), min(16, flen-q0)) of a 16-B chunk at p (16-B aligned)
 __device__ __forceinline__ void pb_store_chunk(uint8_t *p, uint32_t o0, uint32_t o1, uint32_t o2, uint32_t o3, int q0,
                                                int flen)
@@ -919,10 +941,7 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
             }
         }
 
-        uint32_t sum = acc;
-#pragma unroll
-        for (int w = 1; w < G; w <<= 1)
-            sum += __shfl_xor(sum, w, 64);
+        const uint32_t sum = pb_group_sum<G>(acc);
         if ((flags & PBK_L4_CSUM) && lg == 0)
         {
             uint32_t pc = pb_fold(sum);
@@ -1002,28 +1021,6 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
             (t) = now;                                                                                \
         }                                                                                             \
     } while (0)
-
-// Sum over aligned groups of G lanes (G = 8, 16, 32, 64), result in every lane
-// of the group: in-row steps by DPP (no LDS round trip), the rest by swizzle /
-// shuffle.
-template <int G>
-__device__ __forceinline__ uint32_t pb_group_sum(uint32_t v)
-{
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false); // quad_perm [2,3,0,1]
-    if (G == 8)
-        v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F); // xor 4
-    if (G >= 16)
-    {
-        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false); // row_ror:4
-        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false); // row_ror:8
-    }
-    if (G >= 32)
-        v += __shfl_xor(v, 16, 64);
-    if (G >= 64)
-        v += __shfl_xor(v, 32, 64);
-    return v;
-}
 
 template <int G, int RMODE, int WGT>
 __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
