@@ -126,8 +126,9 @@ int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq);
 /* Device time of the frame-build kernels launched since the last call:
  * sum over launches (ms) and launch count (HIP events on the ctx stream). */
 int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches);
-/* Write-only roofline probe: `reps` launches of a non-temporal 16-B/lane
- * fill over `bytes`; returns the mean device time per launch. */
+/* Write-only roofline probe: `reps` launches of each of three 16-B/lane fill
+ * shapes over `bytes` (16 KiB per workgroup plain / non-temporal, 4 KiB per
+ * workgroup plain); returns the fastest shape's mean device time per launch. */
 int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_launch);
 /* Build-kernel tile size chosen for a sequence (bytes per workgroup). */
 int pbgpu_tile_bytes(pbgpu_ctx *ctx, uint16_t seq_idx, uint32_t *tile_bytes);

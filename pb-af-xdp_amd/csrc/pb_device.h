@@ -105,6 +105,13 @@ struct pb_kargs
     unsigned long long *dbg; // PB_TIMING builds only: per-workgroup phase timestamps
     const uint2 *lcg48;     // lcg48[m] = L^(48 m): one 16-B chunk of payload = 48 LCG steps
     uint32_t stail[32];     // small kernel, static payload: payload bytes at frame dwords p0.. (p0 = (hl-2)/4)
+    // XCD-owned small kernel (pb_xsmall_kernel), frame lengths dividing 4096: pages of 4 KiB hold
+    // 1 << xs_fp_shift frames; a workgroup owns xs_np = 256 >> xs_fp_shift pages
+    uint32_t xs_fp_shift;
+    uint32_t xs_np;
+    uint32_t xs_nch;        // pages of this launch's stream
+    uint32_t xs_full;       // workgroups [0, xs_full) own XCD-strided pages; the rest take the tail pages in order
+    uint32_t xs_grid;       // >0: launch pb_xsmall_kernel with this many workgroups
 };
 
 __device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)

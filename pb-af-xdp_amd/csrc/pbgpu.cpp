@@ -27,13 +27,19 @@ extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *
                                          hipStream_t st);
 extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *offsets, uint64_t first, uint32_t n,
                                          uint8_t *dst, uint32_t stride, uint16_t *lens, hipStream_t st);
-extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int nt, hipStream_t st);
+extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipStream_t st);
 
 #define PB_JUMP_N (65536 + 256) // entries j = -PB_JNEG .. 65536 + 175
 #define PB_SCAN_FRAMES_PER_BLOCK (256 * 8)
 
 namespace
 {
+
+bool env_is(const char *name, const char *value)
+{
+    const char *e = getenv(name);
+    return e != NULL && strcmp(e, value) == 0;
+}
 
 int verbose()
 {
@@ -643,6 +649,12 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     if (fixed && pls.size() == 1 && minf <= 128)
     {
         K.small_ndw = minf <= 64 ? 16 : 32;
+        if (4096 % minf == 0) // pages of whole frames: pb_xsmall_kernel
+        {
+            while ((minf << K.xs_fp_shift) < 4096)
+                ++K.xs_fp_shift;
+            K.xs_np = 256 >> K.xs_fp_shift;
+        }
         if (!pls[0].random)
         {
             const uint32_t p0 = (K.hl - 2) / 4;
@@ -951,6 +963,19 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     if (n_tiles > 0x7FFFFFFFull)
         return PBGPU_ENOSPC;
     K.n_tiles = (uint32_t)n_tiles;
+    K.xs_grid = 0;
+    if (K.small_ndw && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && !env_is("PBGPU_KERNEL", "linear"))
+    {
+        // XCD-owned 4 KiB pages (pb_xsmall_kernel): groups of 8 workgroups x 4 pages, tail pages in order
+        const uint64_t nch = (K.total_bytes + 4095) / 4096;
+        if (nch < 0x7FFFFFFFull)
+        {
+            K.xs_nch = (uint32_t)nch;
+            const uint32_t np = K.xs_np;
+            K.xs_full = (uint32_t)(nch / (8 * np) * 8);
+            K.xs_grid = K.xs_full + (uint32_t)((nch - (uint64_t)K.xs_full * np + np - 1) / np);
+        }
+    }
     timing_pair tp;
     int rc = timed_pair(ctx, &tp);
     if (rc)
@@ -1198,12 +1223,12 @@ int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_p
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     double best = 1e30;
-    for (int nt = 0; nt < 2; ++nt) // plain and non-temporal stores; report the faster
+    for (int mode = 0; mode < 3; ++mode) // the store shapes of pbk_launch_fill; report the fastest
     {
-        HIPCHK(pbk_launch_fill(buf, bytes, nt, ctx->stream)); // warm-up
+        HIPCHK(pbk_launch_fill(buf, bytes, mode, ctx->stream)); // warm-up
         HIPCHK(hipEventRecord(a, ctx->stream));
         for (uint32_t r = 0; r < reps; ++r)
-            HIPCHK(pbk_launch_fill(buf, bytes, nt, ctx->stream));
+            HIPCHK(pbk_launch_fill(buf, bytes, mode, ctx->stream));
         HIPCHK(hipEventRecord(b, ctx->stream));
         HIPCHK(hipEventSynchronize(b));
         float ms = 0;
@@ -1241,7 +1266,9 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
     else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.small_ndw)
-        snprintf(buf, n, "pb_small_kernel<%u, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
+        snprintf(buf, n, "%s<%u, %u, %s>",
+                 K.xs_np && !env_is("PBGPU_KERNEL", "linear") ? "pb_xsmall_kernel" : "pb_small_kernel",
+                 K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
     else
         snprintf(buf, n, "pb_build_kernel<%s>", K.fixed_len ? "true" : "false");
     return PBGPU_OK;

@@ -524,133 +524,152 @@ __device__ __forceinline__ uint32_t pb_range_mask(int lo, int hi)
     return ge & lt;
 }
 
+// One whole frame of <= 4*NDW bytes in VGPRs (iteration k = first_iter + fidx,
+// sequence.c:433-602): header fields, payload, L4 and IPv4 checksums.
 template <int NDW, int PROTO, bool RANDOM>
-__global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
+__device__ __forceinline__ void pb_small_frame(const pb_kargs &K, uint64_t fidx, uint32_t (&d)[NDW])
 {
     constexpr int HL = PROTO == 6 ? 54 : 42;
     constexpr int P0 = (HL - 2) / 4;                                 // payload byte 0 = byte 2 of dword P0
     constexpr int CDW = PROTO == 17 ? 10 : (PROTO == 6 ? 12 : 9);   // L4 checksum dword
     constexpr int CSH = PROTO == 6 ? 16 : 0;                         // ... and its half
+    const uint32_t flen = K.fixed_len;
+    const uint32_t flags = K.flags;
+    const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + fidx);
+    const uint32_t r0 = pb_rand_r(s);
+    const uint32_t plen = flen - HL;
+    uint32_t h[16];
+    const uint32_t l4tot = pb_header(K, r0, plen, h, pb_range(K, r0));
+#pragma unroll
+    for (int t = 0; t < NDW; ++t)
+        d[t] = t < 16 ? h[t] : 0u;
+
+    if (RANDOM)
+    {
+        // single payload: its draws start from the iteration seed (sequence.c:548-555)
+        const uint32_t a3 = PB_A3, c3 = PB_C3;
+        const int nv = (int)((flags & PBK_LITERAL) ? min(plen, 1u) : plen);
+        uint32_t y0 = pb_step3(s, a3, c3), y1 = pb_step3(y0, a3, c3);
+        uint32_t x = y1;
+        d[P0] |= __builtin_amdgcn_perm(y1, y0, 0x06020C0Cu) & pb_range_mask(HL - 4 * P0, HL + nv - 4 * P0);
+#pragma unroll
+        for (int t = P0 + 1; t < NDW; ++t)
+        {
+            const uint32_t x0 = pb_step3(x, a3, c3), x1 = pb_step3(x0, a3, c3);
+            const uint32_t x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
+            x = x3;
+            d[t] |= pb_pack4(x0, x1, x2, x3) & pb_range_mask(0, HL + nv - 4 * t);
+        }
+    }
+    else
+    {
+#pragma unroll
+        for (int t = P0; t < NDW; ++t)
+            d[t] |= K.stail[t - P0];
+    }
+    // bytes past the frame end
+#pragma unroll
+    for (int t = 0; t < NDW; ++t)
+        d[t] &= pb_range_mask(0, (int)flen - 4 * t);
+
+    // L4 checksum (csum_tcpudp_magic / icmp_csum, sequence.c:569-594)
+    uint32_t sum = d[8] >> 16;
+#pragma unroll
+    for (int t = 9; t < NDW; ++t)
+        sum = pb_add_halves(sum, d[t]);
+    if (PROTO != 1)
+        sum += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((PROTO + l4tot) << 8);
+    const uint32_t c = (flags & PBK_L4_CSUM) ? ((~pb_fold(sum)) & 0xFFFFu) : 0u;
+    d[CDW] |= c << CSH;
+}
+
+// LDS slot swizzle of 8-B / 16-B aligned frame images: 16-B slot sl -> sl ^ ((sl >> 3) & 7),
+// so lanes at a 64-B stride hit distinct banks; readers undo it with the same map.
+__device__ __forceinline__ uint32_t pb_swz(uint32_t sl)
+{
+    return sl ^ ((sl >> 3) & 7u);
+}
+
+// Frame image d[] -> LDS tile at byte offset B (B has the frame's own alignment
+// mod 16): whole 16-B / 8-B / 4-B words where the frame length allows, byte
+// writes at the two ends of a frame that starts or ends inside a dword.
+template <int NDW>
+__device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&d)[NDW], uint32_t B, uint32_t flen)
+{
+    if ((flen & 15u) == 0)
+    {
+        pb_u32x4 *tile16 = reinterpret_cast<pb_u32x4 *>(s_tile);
+        const uint32_t slot0 = B >> 4;
+#pragma unroll
+        for (int t = 0; t < NDW; t += 4)
+            if ((uint32_t)(4 * t) < flen)
+                tile16[pb_swz(slot0 + (t >> 2))] = pb_u32x4{d[t], d[t + 1], d[t + 2], d[t + 3]};
+    }
+    else if ((flen & 7u) == 0)
+    {
+        uint2 *tile8 = reinterpret_cast<uint2 *>(s_tile);
+        const uint32_t q0 = B >> 3;
+#pragma unroll
+        for (int t = 0; t < NDW; t += 2)
+            if ((uint32_t)(4 * t) < flen)
+            {
+                const uint32_t q = q0 + (t >> 1);
+                tile8[(pb_swz(q >> 1) << 1) | (q & 1u)] = make_uint2(d[t], d[t + 1]);
+            }
+    }
+    else if ((flen & 3u) == 0)
+    {
+        const uint32_t w0 = B >> 2;
+#pragma unroll
+        for (int t = 0; t < NDW; ++t)
+            if ((uint32_t)(4 * t) < flen)
+                s_tile[w0 + t] = d[t];
+    }
+    else
+    {
+        // frame starts at byte phase sh of a dword: out dword u = frame bytes [4u - sh, 4u - sh + 4)
+        const uint32_t sh = B & 3u;
+        uint32_t *row = s_tile + (B >> 2);
+        uint8_t *rowb = reinterpret_cast<uint8_t *>(row);
+        const uint32_t end = sh + flen; // row bytes this frame owns: [sh, end)
+#pragma unroll
+        for (int u = 0; u <= NDW; ++u)
+        {
+            if ((uint32_t)(4 * u) < end)
+            {
+                const uint32_t lo = u > 0 ? d[u - 1] : 0u;
+                const uint32_t hi = u < NDW ? d[u] : 0u;
+                const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
+                const uint32_t b0 = u == 0 ? sh : 0u;
+                const uint32_t b1 = end - 4 * u < 4 ? end - 4 * u : 4u;
+                if (b0 == 0 && b1 == 4)
+                    row[u] = v;
+                else
+                    for (uint32_t b = b0; b < b1; ++b)
+                        rowb[4 * u + b] = (uint8_t)(v >> (8 * b));
+            }
+        }
+    }
+}
+
+// Linear form: workgroup b builds frames [256 b, 256 b + 256) and writes their
+// contiguous byte range.  Used when the output is not 4 KiB aligned (and under
+// PBGPU_KERNEL=linear for comparison).
+template <int NDW, int PROTO, bool RANDOM>
+__global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
+{
     __shared__ __attribute__((aligned(16))) uint32_t s_tile[PB_WG * NDW + 8];
     const uint32_t tid = threadIdx.x;
     const uint64_t f0 = (uint64_t)blockIdx.x * PB_WG;
     const uint64_t left = K.n_frames - f0;
     const uint32_t nfr = left < PB_WG ? (uint32_t)left : PB_WG;
     const uint32_t flen = K.fixed_len;
-    const uint32_t flags = K.flags;
 
     if (tid < nfr)
     {
-        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + f0 + tid);
-        const uint32_t r0 = pb_rand_r(s);
-        const uint32_t plen = flen - HL;
-        uint32_t h[16];
-        const uint32_t l4tot = pb_header(K, r0, plen, h, pb_range(K, r0));
         uint32_t d[NDW];
-#pragma unroll
-        for (int t = 0; t < NDW; ++t)
-            d[t] = t < 16 ? h[t] : 0u;
-
-        if (RANDOM)
-        {
-            // single payload: its draws start from the iteration seed (sequence.c:548-555)
-            const uint32_t a3 = PB_A3, c3 = PB_C3;
-            const int nv = (int)((flags & PBK_LITERAL) ? min(plen, 1u) : plen);
-            uint32_t y0 = pb_step3(s, a3, c3), y1 = pb_step3(y0, a3, c3);
-            uint32_t x = y1;
-            d[P0] |= __builtin_amdgcn_perm(y1, y0, 0x06020C0Cu) & pb_range_mask(HL - 4 * P0, HL + nv - 4 * P0);
-#pragma unroll
-            for (int t = P0 + 1; t < NDW; ++t)
-            {
-                const uint32_t x0 = pb_step3(x, a3, c3), x1 = pb_step3(x0, a3, c3);
-                const uint32_t x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
-                x = x3;
-                d[t] |= pb_pack4(x0, x1, x2, x3) & pb_range_mask(0, HL + nv - 4 * t);
-            }
-        }
-        else
-        {
-#pragma unroll
-            for (int t = P0; t < NDW; ++t)
-                d[t] |= K.stail[t - P0];
-        }
-        // bytes past the frame end
-#pragma unroll
-        for (int t = 0; t < NDW; ++t)
-            d[t] &= pb_range_mask(0, (int)flen - 4 * t);
-
-        // L4 checksum (csum_tcpudp_magic / icmp_csum, sequence.c:569-594)
-        uint32_t sum = d[8] >> 16;
-#pragma unroll
-        for (int t = 9; t < NDW; ++t)
-            sum = pb_add_halves(sum, d[t]);
-        if (PROTO != 1)
-            sum += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((PROTO + l4tot) << 8);
-        const uint32_t c = (flags & PBK_L4_CSUM) ? ((~pb_fold(sum)) & 0xFFFFu) : 0u;
-        d[CDW] |= c << CSH;
-
-        // frame -> LDS tile at byte offset tid * flen.  16/8-B aligned frames go
-        // through an XOR swizzle of the 16-B slots (slot ^ (slot >> 3) & 7) so
-        // lanes at a 64-B stride hit distinct banks; the copy-out undoes it.
-        const uint32_t B = tid * flen;
-        if ((flen & 15u) == 0)
-        {
-            pb_u32x4 *tile16 = reinterpret_cast<pb_u32x4 *>(s_tile);
-            const uint32_t slot0 = tid * (flen >> 4);
-#pragma unroll
-            for (int t = 0; t < NDW; t += 4)
-                if ((uint32_t)(4 * t) < flen)
-                {
-                    const uint32_t sl = slot0 + (t >> 2);
-                    tile16[sl ^ ((sl >> 3) & 7u)] = pb_u32x4{d[t], d[t + 1], d[t + 2], d[t + 3]};
-                }
-        }
-        else if ((flen & 7u) == 0)
-        {
-            uint2 *tile8 = reinterpret_cast<uint2 *>(s_tile);
-            const uint32_t q0 = tid * (flen >> 3);
-#pragma unroll
-            for (int t = 0; t < NDW; t += 2)
-                if ((uint32_t)(4 * t) < flen)
-                {
-                    const uint32_t q = q0 + (t >> 1);
-                    const uint32_t sl = q >> 1;
-                    tile8[((sl ^ ((sl >> 3) & 7u)) << 1) | (q & 1u)] = make_uint2(d[t], d[t + 1]);
-                }
-        }
-        else if ((flen & 3u) == 0)
-        {
-            const uint32_t w0 = tid * (flen >> 2);
-#pragma unroll
-            for (int t = 0; t < NDW; ++t)
-                if ((uint32_t)(4 * t) < flen)
-                    s_tile[w0 + t] = d[t];
-        }
-        else
-        {
-            // frame starts at byte phase sh of a dword: out dword u = frame bytes [4u - sh, 4u - sh + 4)
-            const uint32_t sh = B & 3u;
-            uint32_t *row = s_tile + (B >> 2);
-            uint8_t *rowb = reinterpret_cast<uint8_t *>(row);
-            const uint32_t end = sh + flen; // row bytes this frame owns: [sh, end)
-#pragma unroll
-            for (int u = 0; u <= NDW; ++u)
-            {
-                if ((uint32_t)(4 * u) < end)
-                {
-                    const uint32_t lo = u > 0 ? d[u - 1] : 0u;
-                    const uint32_t hi = u < NDW ? d[u] : 0u;
-                    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
-                    const uint32_t b0 = u == 0 ? sh : 0u;
-                    const uint32_t b1 = end - 4 * u < 4 ? end - 4 * u : 4u;
-                    if (b0 == 0 && b1 == 4)
-                        row[u] = v;
-                    else
-                        for (uint32_t b = b0; b < b1; ++b)
-                            rowb[4 * u + b] = (uint8_t)(v >> (8 * b));
-                }
-            }
-        }
+        pb_small_frame<NDW, PROTO, RANDOM>(K, f0 + tid, d);
+        pb_small_put<NDW>(s_tile, d, tid * flen, flen);
     }
     __syncthreads();
 
@@ -661,8 +680,7 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
     const bool swz = (flen & 7u) == 0;
     for (uint32_t c = tid; c < nchunks; c += PB_WG)
     {
-        const uint32_t sl = swz ? (c ^ ((c >> 3) & 7u)) : c;
-        pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[sl];
+        pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[swz ? pb_swz(c) : c];
         if (16 * c + 16 > tile_bytes) // last chunk of the stream: zero the tail
         {
 #pragma unroll
@@ -672,6 +690,76 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
         pb_st16(out + 16 * c, v);
     }
     if (blockIdx.x == 0 && tid == 0)
+    {
+        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
+        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+    }
+}
+
+// XCD-owned form, for frame lengths that divide 4096 (64-B configs[1] frames,
+// 128-B frames).  The output stream (4 KiB aligned) is cut into 4 KiB pages of
+// fp = 4096 / flen whole frames; workgroup b, which the dispatcher deals to XCD
+// b % 8, owns pages ((b / 8) * np + i) * 8 + b % 8, i < np = 256 / fp, so every
+// XCD writes only the pages of one residue class mod 8.  Measured on MI355X
+// (tools/wbench.hip, profiles/r01/wbench): plain 16-B fills of 256-thread
+// workgroups with 4 stores per lane reach 6.0 TB/s over linear 16 KiB blocks and
+// 6.6 TB/s with this page ownership; 8 KiB pages, or 4 KiB pages off the 4 KiB
+// address grid, lose the gain.  Built here: 64-B UDP 0.35 -> 0.32 ms per 2 GiB.
+// Lengths that do not divide 4096 cut frames at page edges; building those
+// frames in both owners measured slower than the linear form (60-B TCP 0.37 vs
+// 0.345 ms, 98-B ICMP 0.70 vs 0.64), so they keep pb_small_kernel.
+#define PB_XPG 4096                  // page bytes
+#define PB_XREG (PB_XPG + 256)       // LDS bytes per page region (128 B slack either side)
+#define PB_XNP_MAX 8                 // pages per workgroup: 4 (64-B frames) or 8 (128-B)
+
+template <int NDW, int PROTO, bool RANDOM>
+__global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[(NDW == 16 ? 4 : PB_XNP_MAX) * PB_XREG / 4];
+    const uint32_t tid = threadIdx.x, b = blockIdx.x;
+    const uint32_t flen = K.fixed_len;
+    const uint32_t np = K.xs_np;
+    const uint64_t T = K.total_bytes;
+    uint32_t c0, cs;
+    if (b < K.xs_full)
+        c0 = (b >> 3) * (np * 8) + (b & 7u), cs = 8;
+    else
+        c0 = K.xs_full * np + (b - K.xs_full) * np, cs = 1;
+
+    // page i of the workgroup is frames [c_i * fp, (c_i + 1) * fp)
+    {
+        const uint32_t fps = K.xs_fp_shift; // fp = 1 << fps
+        const uint32_t i = tid >> fps, j = tid & ((1u << fps) - 1u);
+        const uint64_t f = ((uint64_t)(c0 + i * cs) << fps) + j;
+        if (f < K.n_frames)
+        {
+            uint32_t d[NDW];
+            pb_small_frame<NDW, PROTO, RANDOM>(K, f, d);
+            pb_small_put<NDW>(s_tile, d, i * PB_XREG + 128 + j * flen, flen);
+        }
+    }
+    __syncthreads();
+
+    // page i -> HBM: one 16-B store per lane per page
+#pragma unroll
+    for (uint32_t i = 0; i < (NDW == 16 ? 4u : PB_XNP_MAX); ++i)
+    {
+        const uint32_t c = c0 + i * cs;
+        const uint64_t o = (uint64_t)c * PB_XPG + 16 * tid;
+        if (i < np && c < K.xs_nch && o < T)
+        {
+            const uint32_t sl = (i * PB_XREG + 128) / 16 + tid;
+            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[pb_swz(sl)];
+            if (o + 16 > T) // last chunk of the stream: zero the tail
+            {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
+            }
+            pb_st16(K.out + o, v);
+        }
+    }
+    if (b == 0 && tid == 0)
     {
         atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
         atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
@@ -1376,14 +1464,15 @@ __global__ __launch_bounds__(64) void pb_scatter_slots(const uint8_t *src, const
         d[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
 
-// write-only roofline probe: each workgroup streams 16 KiB as 4 contiguous
-// 4-KiB sweeps of 16-B stores (the store shape of the build kernels)
-template <bool NT>
+// write-only roofline probe: each workgroup streams PER contiguous 4-KiB sweeps
+// of 16-B stores (PER = 4: the linear build kernels' shape; PER = 1: 4 KiB per
+// workgroup, the fastest plain fill measured, tools/wbench.hip)
+template <bool NT, int PER>
 __global__ __launch_bounds__(256) void pb_fill_kernel(pb_u32x4 *dst, uint64_t n16, uint32_t v)
 {
-    const uint64_t b = (uint64_t)blockIdx.x * 1024;
+    const uint64_t b = (uint64_t)blockIdx.x * (256 * PER);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < PER; ++i)
     {
         const uint64_t c = b + i * 256 + threadIdx.x;
         if (c < n16)
@@ -1402,9 +1491,19 @@ template <int NDW, int PROTO>
 static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
 {
     if (K->pl0.random)
-        hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true>), dim3(grid), dim3(PB_WG), 0, st, *K);
+    {
+        if (K->xs_grid)
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), 0, st, *K);
+        else
+            hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true>), dim3(grid), dim3(PB_WG), 0, st, *K);
+    }
     else
-        hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false>), dim3(grid), dim3(PB_WG), 0, st, *K);
+    {
+        if (K->xs_grid)
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false>), dim3(K->xs_grid), dim3(PB_WG), 0, st, *K);
+        else
+            hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false>), dim3(grid), dim3(PB_WG), 0, st, *K);
+    }
 }
 
 template <int NDW>
@@ -1524,13 +1623,18 @@ extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *off
     return hipGetLastError();
 }
 
-extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int nt, hipStream_t st)
+// write-roofline probe shapes: 0 = 16 KiB per workgroup (4 plain 16-B stores per lane),
+// 1 = the same with non-temporal stores, 2 = 4 KiB per workgroup (one plain store per lane)
+extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipStream_t st)
 {
     const uint64_t n16 = bytes / 16;
-    const uint32_t grid = (uint32_t)((n16 + 1023) / 1024);
-    if (nt)
-        hipLaunchKernelGGL(pb_fill_kernel<true>, dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+    const uint32_t per = mode == 2 ? 1 : 4;
+    const uint32_t grid = (uint32_t)((n16 + 256 * per - 1) / (256 * per));
+    if (mode == 0)
+        hipLaunchKernelGGL((pb_fill_kernel<false, 4>), dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+    else if (mode == 1)
+        hipLaunchKernelGGL((pb_fill_kernel<true, 4>), dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
     else
-        hipLaunchKernelGGL(pb_fill_kernel<false>, dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+        hipLaunchKernelGGL((pb_fill_kernel<false, 1>), dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
     return hipGetLastError();
 }

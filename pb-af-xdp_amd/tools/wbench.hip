@@ -99,6 +99,89 @@ __global__ __launch_bounds__(256) void fill_dword(uint32_t *dst)
         __builtin_nontemporal_store((uint32_t)i, base + i * 256 + threadIdx.x);
 }
 
+
+// persistent: grid of G blocks; block b writes chunks b, b+G, ... of CH bytes (16 B per lane per store)
+template <int WG, int PER>
+__global__ __launch_bounds__(WG) void fill_chunk(uint8_t *dst, uint64_t nchunks)
+{
+    for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x)
+    {
+        uint8_t *base = dst + c * (uint64_t)WG * PER * 16;
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+        {
+            u32x4 v = {(uint32_t)c, (uint32_t)i, 2u, 3u};
+            *(u32x4 *)(base + ((uint64_t)i * WG + threadIdx.x) * 16) = v;
+        }
+    }
+}
+
+// one-shot blocks of WG threads, PER 16-B stores each
+template <int WG, int PER>
+__global__ __launch_bounds__(WG) void fill_wg(uint8_t *dst)
+{
+    uint8_t *base = dst + (uint64_t)blockIdx.x * WG * PER * 16;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+    {
+        u32x4 v = {(uint32_t)blockIdx.x, (uint32_t)i, 2u, 3u};
+        *(u32x4 *)(base + ((uint64_t)i * WG + threadIdx.x) * 16) = v;
+    }
+}
+
+// one-shot blocks, wave-major order: wave w writes its own contiguous PER KiB
+template <int WG, int PER>
+__global__ __launch_bounds__(WG) void fill_wave(uint8_t *dst)
+{
+    const uint32_t w = threadIdx.x / 64, l = threadIdx.x % 64;
+    uint8_t *base = dst + (uint64_t)blockIdx.x * WG * PER * 16 + (uint64_t)w * PER * 1024;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+    {
+        u32x4 v = {(uint32_t)blockIdx.x, (uint32_t)i, 2u, 3u};
+        *(u32x4 *)(base + ((uint64_t)i * 64 + l) * 16) = v;
+    }
+}
+
+// XCD-aware: block b (dealt to XCD b % 8) writes PER chunks of CH bytes, chunk index ((b/8)*PER + i)*8 + (b+ROT)%8
+template <int WG, int PER, int CH, int ROT>
+__global__ __launch_bounds__(WG) void fill_xcd(uint8_t *dst)
+{
+    const uint32_t b = blockIdx.x;
+    constexpr int SPC = CH / (WG * 16); // stores per chunk per lane
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+    {
+        const uint64_t c = ((uint64_t)(b >> 3) * PER + i) * 8 + ((b + ROT) & 7);
+#pragma unroll
+        for (int s = 0; s < SPC; ++s)
+        {
+            u32x4 v = {b, (uint32_t)i, 2u, 3u};
+            *(u32x4 *)(dst + c * CH + ((uint64_t)s * WG + threadIdx.x) * 16) = v;
+        }
+    }
+}
+
+// XCD-aware with arbitrary chunk bytes CB (multiple of 16, <= WG*16*SPC): chunk c at c*CB + off
+template <int WG, int PER, int SPC>
+__global__ __launch_bounds__(WG) void fill_xcdb(uint8_t *dst, uint32_t CB, uint32_t off)
+{
+    const uint32_t b = blockIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+    {
+        const uint64_t c = ((uint64_t)(b >> 3) * PER + i) * 8 + (b & 7);
+#pragma unroll
+        for (int s = 0; s < SPC; ++s)
+        {
+            const uint32_t o = (s * WG + threadIdx.x) * 16;
+            u32x4 v = {b, (uint32_t)i, 2u, 3u};
+            if (o < CB)
+                *(u32x4 *)(dst + off + c * CB + o) = v;
+        }
+    }
+}
+
 template <typename F>
 double timeit(F launch, int reps)
 {
@@ -126,6 +209,43 @@ int main(int argc, char **argv)
     auto rep = [&](const char *name, double ms) {
         printf("%-40s %8.3f ms  %8.1f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
     };
+    if (argc > 2)
+    {
+        // size / shape sweep of plain 16-B stores (argv[2] = any): which shape and buffer size reach the write ceiling
+#define WG_CASE(WG, PER)                                                                                           \
+    {                                                                                                              \
+        char nm[64];                                                                                               \
+        snprintf(nm, 64, "wg=%d per=%d", WG, PER);                                                                 \
+        rep(nm, timeit([&] { hipLaunchKernelGGL((fill_wg<WG, PER>), dim3(bytes / (WG * PER * 16)), dim3(WG), 0, 0, buf); }, reps)); \
+    }
+        WG_CASE(256, 1) WG_CASE(256, 4)
+#define XC_CASE(WG, PER, CH, ROT)                                                                                  \
+    {                                                                                                              \
+        char nm[64];                                                                                               \
+        snprintf(nm, 64, "xcd wg=%d per=%d ch=%d rot=%d", WG, PER, CH, ROT);                                        \
+        rep(nm, timeit([&] { hipLaunchKernelGGL((fill_xcd<WG, PER, CH, ROT>), dim3(bytes / ((uint64_t)PER * CH)), dim3(WG), 0, 0, buf); }, reps)); \
+    }
+        XC_CASE(256, 4, 4096, 0)
+#define XB_CASE(WG, PER, SPC, CB, OFF)                                                                             \
+    {                                                                                                              \
+        char nm[64];                                                                                               \
+        snprintf(nm, 64, "xcdb wg=%d per=%d cb=%d off=%d", WG, PER, CB, OFF);                                      \
+        rep(nm, timeit([&] { hipLaunchKernelGGL((fill_xcdb<WG, PER, SPC>), dim3((bytes - 65536) / ((uint64_t)PER * CB)), dim3(WG), 0, 0, buf, (uint32_t)CB, (uint32_t)OFF); }, reps)); \
+    }
+        XB_CASE(256, 4, 1, 4096, 0) XB_CASE(256, 4, 1, 4096, 256) XB_CASE(256, 4, 1, 4096, 1024) XB_CASE(256, 4, 1, 4096, 2048)
+        XB_CASE(256, 4, 1, 3840, 0) XB_CASE(256, 4, 1, 3584, 0) XB_CASE(256, 4, 2, 6144, 0) XB_CASE(256, 4, 2, 5120, 0)
+        XB_CASE(256, 1, 1, 3840, 0) XB_CASE(256, 1, 1, 4096, 2048) XB_CASE(256, 1, 2, 6000, 0) XB_CASE(256, 2, 2, 6000, 0)
+        XB_CASE(256, 1, 4, 12288, 0) XB_CASE(256, 2, 4, 12288, 0) XB_CASE(256, 1, 4, 16384, 0)
+#define CH_CASE(WG, PER, G)                                                                                        \
+    {                                                                                                              \
+        char nm[64];                                                                                               \
+        snprintf(nm, 64, "persistent wg=%d per=%d grid=%d", WG, PER, G);                                           \
+        rep(nm, timeit([&] { hipLaunchKernelGGL((fill_chunk<WG, PER>), dim3(G), dim3(WG), 0, 0, buf, bytes / (WG * PER * 16)); }, reps)); \
+    }
+        CH_CASE(1024, 8, 256)
+        CK(hipFree(buf));
+        return 0;
+    }
     const uint64_t n16 = bytes / 16;
     for (int g : {1024, 2048, 4096, 8192, 16384, 65536})
     {

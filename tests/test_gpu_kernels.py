@@ -16,16 +16,17 @@ from pbgpu import GpuContext, Sequence
 pytestmark = pytest.mark.gpu
 
 SHAPES = [
-    ("gpf", {"PBGPU_KERNEL": "gpf"}, ("pb_gpf_kernel", "pb_small_kernel")),
+    ("gpf", {"PBGPU_KERNEL": "gpf"}, ("pb_gpf_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
+    ("linear_small", {"PBGPU_KERNEL": "linear"}, ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel")),
     ("tile", {"PBGPU_KERNEL": "tile"}, ("pb_build_kernel",)),
     ("stage_g8_wgf5", {"PBGPU_KERNEL": "stage", "PBGPU_G": "8", "PBGPU_WGF": "5"},
-     ("pb_stage_kernel<8", "pb_small_kernel")),
+     ("pb_stage_kernel<8", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("stage_g64_kb4", {"PBGPU_KERNEL": "stage", "PBGPU_G": "64", "PBGPU_STAGE_KB": "4"},
-     ("pb_stage_kernel<64", "pb_small_kernel")),
+     ("pb_stage_kernel<64", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("stage_wave", {"PBGPU_KERNEL": "stage", "PBGPU_WGT": "64", "PBGPU_WGF": "24"},
-     ("pb_stage_kernel", "pb_small_kernel")),
+     ("pb_stage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("stage_g32_kb36", {"PBGPU_KERNEL": "stage", "PBGPU_G": "32", "PBGPU_STAGE_KB": "36"},
-     ("pb_stage_kernel<32", "pb_small_kernel")),
+     ("pb_stage_kernel<32", "pb_xsmall_kernel", "pb_small_kernel<")),
 ]
 
 
@@ -88,3 +89,29 @@ def test_huge_frames(ctx, plen):
     cfg["payloads"] = [{"length": {"min": 30000, "max": plen}}]
     kern = _check(ctx, cfg, 7, 96)
     assert kern.startswith("pb_gpf_kernel"), kern
+
+
+# Small frames: lengths dividing 4096 (64, 128 B) take pb_xsmall_kernel (4 KiB
+# pages owned per XCD), the others pb_small_kernel.  Frame lengths 42..128 B
+# cover every LDS placement mode (16-B, 8-B, 4-B and byte-aligned frames); the
+# frame counts hit < 1 page, exactly 32 pages (one full group of 8 workgroups),
+# one frame past it, and a ragged tail after several full groups.
+XS_LENS = [42, 43, 60, 64, 72, 96, 98, 106, 127, 128]
+XS_COUNTS = [1, 5, 200, 2048, 2049, 2 * 2048 * 5 + 77]
+
+
+@pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
+@pytest.mark.parametrize("flen", XS_LENS)
+def test_small_frames_pages(ctx, proto, flen):
+    hl = 54 if proto == "tcp" else 42
+    if flen < hl or (proto == "icmp" and flen == hl):
+        pytest.skip("shorter than the headers / empty static payload")
+    cfg = copy.deepcopy(pc.get({"udp": "c2_udp_64", "tcp": "c4_tcp_syn", "icmp": "c5_icmp_echo"}[proto]))
+    if proto == "icmp":  # static payload
+        cfg["payloads"] = [{"exact": " ".join("%02X" % (i * 7 & 255) for i in range(flen - hl))}]
+    else:
+        cfg["payloads"] = [{"length": {"min": flen - hl, "max": flen - hl}}]
+    for n in XS_COUNTS:
+        n = max(1, n * 64 // flen)  # page counts as named above at every length
+        kern = _check(ctx, cfg, 1000003 + n, n)
+        assert kern.startswith("pb_xsmall_kernel" if 4096 % flen == 0 else "pb_small_kernel<"), kern
