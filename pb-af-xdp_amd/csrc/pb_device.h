@@ -20,7 +20,7 @@
 #define PB_IMG_STRIDE 20                   // dwords per frame image row in LDS (16 used + pad: conflict-free b128 rows)
 #define PB_JNEG 80                         // jump table starts at j = -80
 #define PB_STAGE_L48 72                    // lcg48 entries the staged kernel keeps in LDS (> 4 + 64)
-#define PB_STAGE_LDS(wgf) ((size_t)(wgf) * (16 + 7) * 4 + 4 + PB_STAGE_L48 * 8) // its LDS besides the stage
+#define PB_STAGE_LDS(wgf) ((size_t)(wgf) * (16 + 8) * 4 + 4 + PB_STAGE_L48 * 8) // its LDS besides the stage
 #define PB_LCG48_N 4200                    // lcg48[m] = L^(48 m), m < 4200 (> 16-B chunks of a 64 KiB frame)
 
 // glibc LCG

@@ -1124,7 +1124,8 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
     uint32_t *const s_z = s_hs + WF;       // LCG state at the frame's first 16-B chunk
     uint32_t *const s_nv = s_z + WF;       // nvalid | random << 31
     uint32_t *const s_src = s_nv + WF;     // blob offset (static payload)
-    uint32_t *const s_win = s_src + WF;    // s_win[w]: first frame of window w, [nwin] = nfr
+    uint32_t *const s_gs = s_src + WF;     // word sum of the drawn bytes B writes outside the payload
+    uint32_t *const s_win = s_gs + WF;     // s_win[w]: first frame of window w, [nwin] = nfr
 
     const uint32_t tid = threadIdx.x;
     const uint32_t flags = K.flags;
@@ -1192,6 +1193,36 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
         s_z[tid] = P.random ? jt.x * P.st0 + jt.y : 0u;
         s_nv[tid] = P.nvalid | (P.random << 31);
         s_src[tid] = P.blob_off;
+        // B writes every payload chunk whole and unmasked: the first one also holds
+        // header bytes [j0, 0) of this frame, the last one bytes [nvalid, jl + 16)
+        // that belong to the next frame's header (both rewritten by C).  Their LCG
+        // bytes enter B's word sum (output alignment: byte p of a chunk weighs
+        // 2^(8 (p & 1))); their sum is taken here once, one lane per frame, and
+        // subtracted after B's reduction.  Static payloads read zero padding there;
+        // the literal rule keeps B's byte masks.
+        uint32_t gs = 0;
+        if (P.random && !(flags & PBK_LITERAL))
+        {
+            const int s0 = (int)(my_r & 15u);
+            const int j0 = 16 * ((s0 + hl) >> 4) - s0 - hl; // (-16, 0]
+            const int jl = 16 * ((s0 + (int)flen - 1) >> 4) - s0 - hl;
+            const uint2 ja = K.jump[PB_JNEG + j0];
+            uint32_t x = ja.x * P.st0 + ja.y;
+            for (int p = 0; p < -j0; ++p)
+            {
+                gs += ((x >> 16) & 0xFFu) << (8 * (p & 1));
+                x = pb_step3(x, PB_A3, PB_C3);
+            }
+            const int t0 = (int)P.nvalid > jl ? (int)P.nvalid : jl;
+            const uint2 jb = K.jump[PB_JNEG + t0];
+            x = jb.x * P.st0 + jb.y;
+            for (int p = t0 - jl; p < 16; ++p)
+            {
+                gs += ((x >> 16) & 0xFFu) << (8 * (p & 1));
+                x = pb_step3(x, PB_A3, PB_C3);
+            }
+        }
+        s_gs[tid] = gs;
     }
 #pragma unroll
     for (uint32_t i = 0; i < (PB_STAGE_L48 + WGT - 1) / WGT; ++i)
@@ -1217,6 +1248,7 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
     constexpr uint32_t NGW = WGT / G; // frames in flight per workgroup
     const uint32_t grp = tid / G, lg = tid % G;
     const uint2 MG = s_l48[G];
+    const bool lit = (flags & PBK_LITERAL) != 0;
     for (uint32_t w = 0; w < nwin; ++w)
     {
         const uint32_t sb = s_win[w], se = s_win[w + 1];
@@ -1250,10 +1282,10 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
                 const int j0 = (int)(16 * m) - s0 - hl; // payload index of the chunk's first byte
                 uint32_t o0, o1, o2, o3;
                 pb_chunk_payload(K, rnd, x, src, j0, 0, 16, o0, o1, o2, o3);
-                if (j0 < 0 || j0 + 16 > nvalid)
+                if (lit && (j0 < 0 || j0 + 16 > nvalid))
                 {
-                    // chunk bytes outside the drawn payload: zero (past nvalid, literal
-                    // rule) or header bytes of this / the next frame, rewritten by C
+                    // literal rule: chunk bytes outside the drawn payload are zero (past
+                    // nvalid) or header bytes of this / the next frame, rewritten by C
                     const int lo = -j0, hi = nvalid - j0;
                     o0 &= pb_range_mask(lo, hi);
                     o1 &= pb_range_mask(lo - 4, hi - 4);
@@ -1268,7 +1300,7 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
             acc = pb_group_sum<G>(acc);
             if ((flags & PBK_L4_CSUM) && lg == 0)
             {
-                uint32_t pc = pb_fold(acc);
+                uint32_t pc = pb_fold(acc - s_gs[fr]);
                 if (r & 1u) // chunk sums were taken in output alignment
                     pc = pb_bswap16(pc);
                 const uint32_t c = (~pb_fold(pb_fold(s_hs[fr]) + pc)) & 0xFFFFu;
