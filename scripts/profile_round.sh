@@ -6,12 +6,12 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_round
 rm -rf $OUT; mkdir -p $OUT
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench_trace -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-seconds 2 > $OUT/bench_trace.log 2>&1 || { echo TRACE_FAIL; tail -5 $OUT/bench_trace.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench_trace -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-seconds 2 > $OUT/bench_trace.log 2>&1 || { echo TRACE_FAIL; tail -5 $OUT/bench_trace.log; exit 1; }
 grep '^{"metric"' $OUT/bench_trace.log > $OUT/bench_under_trace.json
 python3 scripts/trace_summary.py $OUT/bench_trace/run_kernel_trace.csv $OUT/kernel_trace_summary.json
 for cfg in c2_udp_64 c2_udp_1500 c3_udp_var c4_tcp_syn c5_icmp_echo; do
   P=33554432; [ $cfg = c3_udp_var ] && P=16777216
-  B="python3 bench.py --steps 5 --warmup 2 --no-variants --cpu-seconds 0 --config $cfg --packets $P"
+  B="python3 bench.py --steps 5 --warmup 2 --ramp-seconds 0 --no-variants --cpu-seconds 0 --config $cfg --packets $P"
   for grp in "WRITE_SIZE" "FETCH_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
     tag=$(echo $grp | cut -d' ' -f1 | tr 'A-Z' 'a-z')
     timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_${cfg}_$tag -o run -- $B > $OUT/pmc_${cfg}_$tag.log 2>&1 || { echo "PMC_FAIL $cfg $grp"; tail -3 $OUT/pmc_${cfg}_$tag.log; exit 1; }
