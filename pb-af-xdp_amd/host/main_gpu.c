@@ -6,8 +6,9 @@
  * then optind = 0 and the AF_XDP options of cmd_line.c plus this build's GPU
  * options), the first-sequence override (-z, README.md:101-151), sequences
  * run in order through seq_send(), shutdown_prog() on exit or SIGINT/SIGTERM.
- * JSON config files (-c) need PB-Common + json-c, which are not in this
- * build: use -z, or the Python loader (pb-af-xdp_amd/pbgpu.py).
+ * The JSON config (-c, default /etc/pcktbatch/conf.json) is read first and the
+ * -z overrides are applied to its first sequence afterwards, as main.c:90-103
+ * does with PB-Common's parse_config() / parse_cli() (host/config_json.c).
  * Frames go to the TX hook: a pcap file with --pcap, otherwise counted.
  */
 #include <getopt.h>
@@ -17,6 +18,7 @@
 #include <string.h>
 
 #include "cmd_line.h"
+#include "config_json.h"
 #include "sequence_gpu.h"
 
 typedef struct cmd_line
@@ -164,7 +166,7 @@ static void parse_common(int argc, char **argv, cmd_line_t *cmd, pb_sequence_t *
 static void print_cmd_help(void)
 {
     fprintf(stdout, "Usage: pcktbatch-gpu -c <configfile> | -z [overrides] [-v -l -h] [AF_XDP/GPU options]\n\n"
-                    "-c --cfg => Path to the config file (JSON configs: use the Python loader).\n"
+                    "-c --cfg => Path to the config file (default /etc/pcktbatch/conf.json).\n"
                     "-l --list => Print basic information about sequences.\n"
                     "-v --verbose => Provide verbose output.\n"
                     "-h --help => Print out help menu and exit program.\n"
@@ -182,8 +184,20 @@ int main(int argc, char **argv)
         return EXIT_FAILURE;
     for (int i = 0; i < PB_MAX_SEQUENCES; ++i)
         clear_sequence(cfg, i);
+    /* getopt permutes argv (the AF_XDP pass moves the values of options it does not
+     * know); the -z overrides are re-read later from this untouched copy */
+    char **argv_cli = (char **)malloc(((size_t)argc + 1) * sizeof *argv_cli);
+    if (argv_cli == NULL)
+        return EXIT_FAILURE;
+    memcpy(argv_cli, argv, ((size_t)argc + 1) * sizeof *argv_cli);
     const char *iface = NULL;
-    parse_common(argc, argv, &cmd, &cfg->seq[0], &iface);
+    {
+        /* first pass for the common flags only (main.c:30); the -z overrides are
+         * applied after the config file */
+        pb_sequence_t scratch;
+        memset(&scratch, 0, sizeof scratch);
+        parse_common(argc, argv, &cmd, &scratch, &iface);
+    }
     if (cmd.help)
     {
         print_cmd_help();
@@ -195,19 +209,27 @@ int main(int argc, char **argv)
     parse_cmd_line_af_xdp(&cmd_af_xdp, argc, argv);
     pb_set_verbose(cmd.verbose);
 
+    if (cmd.config == NULL) /* main.c:51-61 */
+    {
+        cmd.config = "/etc/pcktbatch/conf.json";
+        if (cmd.verbose)
+            fprintf(stdout, "No config specified. Using default: %s.\n", cmd.config);
+    }
     int seq_cnt = 0;
     if (cmd.cli)
-    {
         fprintf(stdout, "Using command line...\n");
-        seq_cnt = 1;
-        cfg->interface = iface;
-    }
-    else
-    {
-        fprintf(stderr, "No -z/--cli sequence given (JSON config '%s' needs the Python loader: "
-                        "pb-af-xdp_amd/pbgpu.py Sequence.from_config).\n",
-                cmd.config ? cmd.config : "/etc/pcktbatch/conf.json");
+    const int prc = pb_parse_config(cmd.config, cfg, &seq_cnt, !cmd.cli); /* main.c:94 */
+    if (prc != 0 && !cmd.cli)
         return EXIT_FAILURE;
+    if (cmd.cli) /* parse_cli(): the overrides of the first sequence (main.c:96-103) */
+    {
+        optind = 0;
+        iface = NULL;
+        parse_common(argc, argv_cli, &cmd, &cfg->seq[0], &iface);
+        if (iface)
+            cfg->interface = iface;
+        if (seq_cnt < 1)
+            seq_cnt = 1;
     }
     if (cmd.list)
     {
@@ -245,5 +267,7 @@ int main(int argc, char **argv)
     pb_pcap_close(pcap);
     const int err = pb_last_error();
     free(cfg);
+    free(argv_cli);
+    pb_config_free();
     return err ? EXIT_FAILURE : EXIT_SUCCESS;
 }

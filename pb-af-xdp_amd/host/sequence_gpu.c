@@ -11,6 +11,7 @@
  */
 #define _GNU_SOURCE
 #include "sequence_gpu.h"
+#include "mac.h"
 
 #include <errno.h>
 #include <pthread.h>
@@ -43,6 +44,7 @@ void pb_request_stop(void)
 typedef struct worker_arg
 {
     pb_sequence_t seq;
+    const char *device; /* the interface seq_send() was given (MAC discovery) */
     uint16_t seq_idx;
     int gpu;
     int shard;
@@ -103,7 +105,33 @@ static void *gpu_worker(void *p)
     }
     pb_rules_t rules = {w->cmd.literal_payload ? PB_PAYLOAD_LITERAL : PB_PAYLOAD_STREAM,
                         w->cmd.single_fold ? PB_FOLD_SINGLE : PB_FOLD_FULL};
-    if ((rc = pbgpu_load_sequence(ctx, w->seq_idx, seq, NULL, NULL, &rules, w->cmd.seed_base)) != 0)
+    /* MACs: a zero source MAC is the device's, a zero destination MAC the default
+     * gateway's (sequence.c:111-136) */
+    uint8_t smac[6] = {0}, dmac[6] = {0};
+    if (seq->eth.src_mac)
+        sscanf(seq->eth.src_mac, "%hhx:%hhx:%hhx:%hhx:%hhx:%hhx", &smac[0], &smac[1], &smac[2], &smac[3], &smac[4],
+               &smac[5]);
+    if (seq->eth.dst_mac)
+        sscanf(seq->eth.dst_mac, "%hhx:%hhx:%hhx:%hhx:%hhx:%hhx", &dmac[0], &dmac[1], &dmac[2], &dmac[3], &dmac[4],
+               &dmac[5]);
+    static const uint8_t zero[6] = {0};
+    if (memcmp(smac, zero, 6) == 0)
+    {
+        if (pb_get_src_mac_address(w->device, smac) != 0)
+            fprintf(stdout, "[%d] WARNING - Failed to retrieve MAC address for %s.\n", seq_num, w->device);
+        if (memcmp(smac, zero, 6) == 0)
+            fprintf(stdout, "[%d] WARNING - Source MAC address retrieved is 00:00:00:00:00:00.\n", seq_num);
+    }
+    if (memcmp(dmac, zero, 6) == 0)
+        (void)pb_get_gw_mac(dmac);
+    if (verbose)
+    {
+        printf("[%d] Source MAC address => %hhx:%hhx:%hhx:%hhx:%hhx:%hhx.\n", seq_num, smac[0], smac[1], smac[2],
+               smac[3], smac[4], smac[5]);
+        printf("[%d] Destination MAC address => %hhx:%hhx:%hhx:%hhx:%hhx:%hhx.\n", seq_num, dmac[0], dmac[1], dmac[2],
+               dmac[3], dmac[4], dmac[5]);
+    }
+    if ((rc = pbgpu_load_sequence(ctx, w->seq_idx, seq, smac, dmac, &rules, w->cmd.seed_base)) != 0)
     {
         fprintf(stderr, "[%d] Error loading sequence on GPU %d :: %s.\n", seq_num, w->gpu, pbgpu_strerror(rc));
         last_error = rc;
@@ -245,6 +273,7 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
         if (w == NULL)
             break;
         w->seq = seq;
+        w->device = interface;
         w->seq_idx = idx;
         w->gpu = cmd.gpu_first + g;
         w->shard = g;

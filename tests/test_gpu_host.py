@@ -2,6 +2,7 @@
 first-sequence CLI) builds frames through libpbgpu, lands them in UMEM slots
 and writes them to a pcap through the TX hook; the capture must equal the
 oracle's frames for the same sequence and seed stream."""
+import json
 import os
 import struct
 import subprocess
@@ -48,14 +49,40 @@ def test_cli_pcap_equals_oracle(tmp_path, batch):
 
 
 def test_cli_variable_tcp_time_limited(tmp_path):
+    """No --smac on a device that does not exist: the source MAC stays zero with
+    the reference's warnings (sequence.c:111-121)."""
     pcap = tmp_path / "tcp.pcap"
-    cmd = [BIN, "-z", "--interface", "eth0", "--dip", pc.DIP, "--sip", "172.16.0.0/12", "--protocol", "tcp",
-           "--tdport", "80", "--syn", "1", "--pmin", "0", "--pmax", "900", "--maxpckts", "3000", "--delay", "0",
-           "--gpubatch", "1000", "--seed", "7", "--pcap", str(pcap)]
+    cmd = [BIN, "-z", "--interface", "pbnodev0", "--dmac", pc.DMAC, "--dip", pc.DIP, "--sip", "172.16.0.0/12",
+           "--protocol", "tcp", "--tdport", "80", "--syn", "1", "--pmin", "0", "--pmax", "900", "--maxpckts", "3000",
+           "--delay", "0", "--gpubatch", "1000", "--seed", "7", "--pcap", str(pcap)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
+    assert "WARNING - Failed to retrieve MAC address for pbnodev0." in r.stdout
+    assert "WARNING - Source MAC address retrieved is 00:00:00:00:00:00." in r.stdout
     got = read_pcap(pcap)
-    cfg = {"eth": {}, "ip": {"dip": pc.DIP, "ranges": ["172.16.0.0/12"], "protocol": "tcp"},
+    cfg = {"eth": {"dmac": pc.DMAC}, "ip": {"dip": pc.DIP, "ranges": ["172.16.0.0/12"], "protocol": "tcp"},
            "tcp": {"dport": 80, "syn": 1}, "payloads": [{"length": {"min": 0, "max": 900}}]}
     want = ob.frames(Sequence.from_config(cfg), 0, 0, 3000, 7)
     assert got == want
+
+
+def test_json_config_sequences_equal_oracle(tmp_path):
+    """pcktbatch-gpu -c conf.json: three sequences (UDP 64 B, TCP SYN, ICMP echo:
+    the configs[4] mix) run in order through seq_send(); the capture is each
+    sequence's oracle frames in turn (sequence index s in the seed stream)."""
+    seqs = []
+    for name, n in (("c2_udp_64", 3000), ("c4_tcp_syn", 2000), ("c5_icmp_echo", 1000)):
+        c = dict(pc.get(name))
+        c.update({"maxpckts": n, "delay": 0, "block": 1})
+        seqs.append(c)
+    path = tmp_path / "conf.json"
+    path.write_text(json.dumps({"interface": "pbnodev0", "sequences": seqs}))
+    pcap = tmp_path / "mix.pcap"
+    r = subprocess.run([BIN, "-c", str(path), "--gpubatch", "1024", "--seed", "99", "--pcap", str(pcap)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Completed 3 sequences!" in r.stdout
+    want = []
+    for i, c in enumerate(seqs):
+        want += ob.frames(Sequence.from_config(c), i, 0, c["maxpckts"], 99)
+    assert read_pcap(pcap) == want
