@@ -712,9 +712,12 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             // (default 24) KiB.  Measured (profiles/r01/stage): 1500-B frames 5.1 TB/s
             // at G = 16, 16 frames per window (group-per-frame: 4.1); 1024-B 5.2 at 16
             // frames; 9000-B 5.2 at G = 64.
-            // variable-length frames stay on the group-per-frame kernel unless
-            // PBGPU_KERNEL=stage (configs[2]: 3.45 TB/s there, 2.75-3.2 staged)
-            const bool gpf_only = (kern && !strcmp(kern, "gpf")) || (!K.fixed_len && !(kern && !strcmp(kern, "stage")));
+            // variable-length frames: staged with G = 8 (configs[2], 2^23 frames: 1.81-1.86 ms
+            // vs 2.01 on the group-per-frame kernel, since B writes payload chunks
+            // unmasked); PBGPU_KERNEL=gpf forces the group-per-frame kernel.  A flat B
+            // (one list of the window's payload chunks, checksums from LCG-cycle prefix
+            // sums) measured slower: 2.1-2.5 ms
+            const bool gpf_only = kern && !strcmp(kern, "gpf");
             const uint32_t avg = (minf + maxf) / 2;
             const uint32_t npc = (avg - K.hl) / 16 + 2;
             double umax = 0;
@@ -728,7 +731,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                     break;
                 }
             if (!K.fixed_len)
-                sg = 16;
+                sg = 8;
             if (ge && (atoi(ge) == 8 || atoi(ge) == 16 || atoi(ge) == 32 || atoi(ge) == 64))
                 sg = (uint32_t)atoi(ge);
             uint32_t wgt = PB_WG;
