@@ -28,6 +28,8 @@ extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *
 extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *offsets, uint64_t first, uint32_t n,
                                          uint8_t *dst, uint32_t stride, uint16_t *lens, hipStream_t st);
 extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipStream_t st);
+extern "C" hipError_t pbk_launch_scatter_fixed(const uint8_t *src, uint32_t flen, uint32_t n, uint8_t *dst,
+                                               uint32_t stride, hipStream_t st);
 
 #define PB_JUMP_N (65536 + 256) // entries j = -PB_JNEG .. 65536 + 175
 #define PB_SCAN_FRAMES_PER_BLOCK (256 * 8)
@@ -1103,8 +1105,19 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
     {
         if (f->fixed_len > slot_stride)
             return PBGPU_EINVAL;
-        HIPCHK(hipMemcpy2DAsync(dst, slot_stride, f->data + first_frame * f->fixed_len, f->fixed_len, f->fixed_len,
-                                n, hipMemcpyDeviceToHost, ctx->stream));
+        // registered (mapped) UMEM: the GPU stores each frame into its slot over the host
+        // link; otherwise a strided DMA copy (one row per frame)
+        void *dev_dst = NULL;
+        if (hipHostGetDevicePointer(&dev_dst, dst, 0) == hipSuccess && dev_dst != NULL &&
+            !getenv("PBGPU_UMEM_DMA"))
+            HIPCHK(pbk_launch_scatter_fixed(f->data + first_frame * f->fixed_len, f->fixed_len, n, (uint8_t *)dev_dst,
+                                            slot_stride, ctx->stream));
+        else
+        {
+            (void)hipGetLastError();
+            HIPCHK(hipMemcpy2DAsync(dst, slot_stride, f->data + first_frame * f->fixed_len, f->fixed_len,
+                                    f->fixed_len, n, hipMemcpyDeviceToHost, ctx->stream));
+        }
         HIPCHK(hipStreamSynchronize(ctx->stream));
         if (lens_out)
             for (uint32_t i = 0; i < n; ++i)

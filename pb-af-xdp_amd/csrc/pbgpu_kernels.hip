@@ -1496,6 +1496,29 @@ __global__ __launch_bounds__(64) void pb_scatter_slots(const uint8_t *src, const
         d[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
 
+// fixed-length frames -> slots: thread (f, i) stores dword i of frame f (f = gid / dpf)
+// at dst + f * stride; straight over the host link when dst is mapped UMEM
+// (af_xdp.c:211-214 geometry: one frame per 4 KiB slot)
+__global__ __launch_bounds__(256) void pb_scatter_fixed(const uint8_t *src, uint32_t flen, uint32_t dpf, uint64_t n_dw,
+                                                        uint8_t *dst, uint32_t stride)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= n_dw)
+        return;
+    const uint64_t f = g / dpf;
+    const uint32_t i = (uint32_t)(g - f * dpf);
+    const uint8_t *s = src + f * flen + 4 * i;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)s & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
+    const uint32_t v = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+    uint8_t *d = dst + f * stride + 4 * i;
+    if (4 * i + 4 <= flen)
+        *reinterpret_cast<uint32_t *>(d) = v;
+    else
+        for (uint32_t b = 0; 4 * i + b < flen; ++b)
+            d[b] = (uint8_t)(v >> (8 * b));
+}
+
 // write-only roofline probe: each workgroup streams PER contiguous 4-KiB sweeps
 // of 16-B stores (PER = 4: the linear build kernels' shape; PER = 1: 4 KiB per
 // workgroup, the fastest plain fill measured, tools/wbench.hip)
@@ -1645,6 +1668,16 @@ extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *
                        K->counters);
     hipLaunchKernelGGL(pb_len_scan, dim3(nblocks), dim3(256), 0, st, *K, (const unsigned long long *)block_sums,
                        offsets, tile_first, tile_shift);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t pbk_launch_scatter_fixed(const uint8_t *src, uint32_t flen, uint32_t n, uint8_t *dst,
+                                               uint32_t stride, hipStream_t st)
+{
+    const uint32_t dpf = (flen + 3) / 4;
+    const uint64_t n_dw = (uint64_t)n * dpf;
+    hipLaunchKernelGGL(pb_scatter_fixed, dim3((uint32_t)((n_dw + 255) / 256)), dim3(256), 0, st, src, flen, dpf, n_dw,
+                       dst, stride);
     return hipGetLastError();
 }
 

@@ -184,6 +184,33 @@ def test_counters_and_umem_landing(ctx):
     fb.free()
 
 
+@pytest.mark.parametrize("name", ["c2_udp_64", "c4_tcp_syn", "c5_icmp_echo", "c2_udp_1500", "c1_udp_static_106"])
+def test_umem_landing_registered(ctx, name):
+    """Fixed-length frames into registered (mapped) UMEM: the GPU scatter kernel
+    stores every frame into its 4 KiB slot (af_xdp.c:211-214); slot bytes past
+    the frame are untouched."""
+    seq = Sequence.from_config(pc.get(name))
+    ctx.load_sequence(9, seq, pc.SEED_BASE)
+    n = 3000
+    fb = ctx.alloc_frames(*ctx.build_size(9, n))
+    ctx.build(9, 555, n, fb)
+    ctx.sync()
+    want = ob.frames(seq, 9, 555, n, pc.SEED_BASE)
+    umem = np.full(4096 * 1024, 0xEE, dtype=np.uint8)
+    assert ctx.lib.pbgpu_host_register(ctx.h, umem.ctypes.data, umem.nbytes) == 0
+    try:
+        lens = fb.to_umem(umem, 4096, 1000, 1024)
+    finally:
+        ctx.lib.pbgpu_host_unregister(ctx.h, umem.ctypes.data)
+    fb.free()
+    flen = len(want[0])
+    assert (lens == flen).all()
+    slots = umem.reshape(1024, 4096)
+    for j in range(1024):
+        assert slots[j, :flen].tobytes() == want[1000 + j]
+    assert (slots[:, flen:] == 0xEE).all()
+
+
 def test_error_behaviour(ctx):
     seq = Sequence.from_config(pc.get("c2_udp_64"))
     ctx.load_sequence(0, seq, 1)
