@@ -112,7 +112,17 @@ struct pb_kargs
     uint32_t xs_nch;        // pages of this launch's stream
     uint32_t xs_full;       // workgroups [0, xs_full) own XCD-strided pages; the rest take the tail pages in order
     uint32_t xs_grid;       // >0: launch pb_xsmall_kernel with this many workgroups
+    // fixed-length staged kernel (pb_fstage_kernel): frame length a multiple of 4, every
+    // payload random, stream rule; one frame per G-lane group per window of 256 / G frames
+    uint32_t fst_g;         // >0: launch it with G lanes per frame (16, 32, 64)
+    uint32_t fst_wgf;       // frames per workgroup (a multiple of 256 / G, <= 256)
+    uint32_t fst_sb;        // bytes per stage buffer (multiple of 16)
+    uint32_t fst_nbuf;      // stage buffers: 2 (window w + 1 is built while w streams out) or 1
+    uint32_t fst_dbg;       // diagnostics (PBGPU_FST_DBG, wrong output): bit 0 skips payload + headers,
+                            // bit 1 the stores, bit 3 phase A (time decomposition)
 };
+// pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
+#define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)
 
 __device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)
 {

@@ -43,6 +43,12 @@ bool env_is(const char *name, const char *value)
     return e != NULL && strcmp(e, value) == 0;
 }
 
+int env_int(const char *name, int dflt)
+{
+    const char *e = getenv(name);
+    return e != NULL && atoi(e) > 0 ? atoi(e) : dflt;
+}
+
 int verbose()
 {
     static int v = -1;
@@ -781,6 +787,47 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 K.stage_wgt = wgt;
                 K.stage_bytes = sbytes;
             }
+            // fixed-length staged kernel (pb_fstage_kernel): lengths > 128 B that are a
+            // multiple of 4, every payload random, stream rule.  One stage buffer, then two;
+            // G = the smallest of 16, 32, 64 whose stage of 256 / G frames fits 64 KiB with
+            // the per-frame records; 64 frames per workgroup.  Measured on 1500-B frames
+            // (profiles/r01/fstage): 1 buffer G = 16 2.12 ms per 2^23 frames, 2 buffers 2.20,
+            // G = 32 2.21, G = 64 2.35, 32 / 128 frames per workgroup 2.15 / 2.20;
+            // pb_stage_kernel 2.29.  PBGPU_KERNEL=stage / gpf keep the older kernels,
+            // PBGPU_FST_G, PBGPU_FST_WGF, PBGPU_FST_NBUF override the shape.
+            const bool fst_ok = K.fixed_len && minf > 128 && minf % 4 == 0 && K.gpf_rmode == 1 &&
+                                !(flags & PBK_LITERAL) && !gpf_only && !env_is("PBGPU_KERNEL", "stage");
+            if (fst_ok)
+            {
+                const uint32_t eg = (uint32_t)env_int("PBGPU_FST_G", 0);
+                const uint32_t ew = (uint32_t)env_int("PBGPU_FST_WGF", 0);
+                const uint32_t en = (uint32_t)env_int("PBGPU_FST_NBUF", 0);
+                for (uint32_t nb : {1u, 2u})
+                {
+                    if (en && nb != en)
+                        continue;
+                    for (uint32_t gg : {16u, 32u, 64u})
+                    {
+                        if ((eg && gg != eg) || K.hl / 4 >= gg)
+                            continue;
+                        const uint32_t ngw = PB_WG / gg;
+                        uint32_t fw = ew ? ew : 64;
+                        fw = std::max(ngw, std::min<uint32_t>(PB_WG, fw / ngw * ngw));
+                        const uint32_t sb = (ngw * minf + 15) / 16 * 16;
+                        if ((size_t)nb * sb + PB_FST_LDS(fw) <= 64 * 1024)
+                        {
+                            K.fst_g = gg;
+                            K.fst_wgf = fw;
+                            K.fst_sb = sb;
+                            K.fst_nbuf = nb;
+                            K.fst_dbg = (uint32_t)env_int("PBGPU_FST_DBG", 0);
+                            break;
+                        }
+                    }
+                    if (K.fst_g)
+                        break;
+                }
+            }
         }
     }
     // tile: power of two, <= 16 KiB, <= (PB_NF_MAX - 2) frames of minimum length
@@ -985,7 +1032,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     int rc = timed_pair(ctx, &tp);
     if (rc)
         return rc;
-    const bool timing = K.stage_win && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
+    const bool timing = K.stage_win && !K.fst_g && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
     const uint64_t n_wg = K.stage_wgf ? (nf + K.stage_wgf - 1) / K.stage_wgf : 0;
     if (timing)
     {
@@ -1277,7 +1324,9 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
     if (!S.loaded)
         return PBGPU_ENOENT;
     const pb_kargs &K = S.K;
-    if (K.stage_win)
+    if (K.fst_g)
+        snprintf(buf, n, "pb_fstage_kernel<%u, %u>", K.fst_g, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
+    else if (K.stage_win)
         snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);

@@ -153,6 +153,23 @@ __device__ __forceinline__ uint32_t pb_pack4(uint32_t x0, uint32_t x1, uint32_t 
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
+// a * x + c on the low 24 bits of x and a, one v_mad_u32_u24 (a in an SGPR, c in a
+// VGPR: __umul24 with both constants uniform costs a v_and and a v_mov per use)
+__device__ __forceinline__ uint32_t pb_mad24(uint32_t x, uint32_t a, uint32_t c)
+{
+    uint32_t r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(a), "v"(c));
+    return r;
+}
+
+// a uniform value held in a VGPR (one v_mov outside the loops that use it)
+__device__ __forceinline__ uint32_t pb_vgpr(uint32_t s)
+{
+    uint32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+    return v;
+}
+
 // 24-bit LCG step: three rand_r steps folded into one affine map mod 2^24.
 __device__ __forceinline__ uint32_t pb_step3(uint32_t x, uint32_t a3, uint32_t c3)
 {
@@ -1374,6 +1391,213 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
     }
 }
 
+// ---------------- fixed-length staged: pb_fstage_kernel ----------------
+//
+// The configs[1] 1500-B shape (any fixed length > 128 B that is a multiple of 4,
+// every payload random, stream rule) with the per-frame and per-window work of
+// pb_stage_kernel cut down: that kernel runs VALU-bound (PMC: ~80% of the SIMD
+// issue cycles) and spends ~45% of its VALU instructions outside the payload
+// loop (105 per 1500-B frame, 56 in the loop).
+//  * Every frame starts on a dword (flen % 4 == 0) and a window is exactly
+//    NGW = 256 / G frames, so NGW * flen % 16 == 0: every window (and every
+//    workgroup, WF being a multiple of NGW) starts on a 16-B boundary, and a
+//    lane's frame offset, chunk range and LCG entry constant (L^(48 m)) are the
+//    same in every window.
+//  * Lane lg of a group takes the frame's payload chunks nch-1-lg, nch-1-lg-G, ...
+//    in ascending order, so the frame's last chunk (which may also hold the next
+//    frame's first dwords) is lane 0's final chunk, in the wave's final pass:
+//    only it is stored dword-masked.  No two groups then write the same stage
+//    bytes, and the group writes its own header right after its payload (LDS
+//    operations of one wave complete in order): no header pass, one barrier per
+//    window.
+//  * Lane 0's checksum accumulator starts at A's per-frame constant: the header /
+//    pseudo-header word sum minus the generated header bytes of the first payload
+//    chunk (overwritten by the header), so the group reduction is the whole sum.
+//  * Two stage buffers: window w + 1 is generated while window w's stores drain.
+template <int G, bool L4>
+__global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
+{
+    constexpr uint32_t NGW = PB_WG / G; // frames per window
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    const uint32_t SB = K.fst_sb, NB = K.fst_nbuf, WF = K.fst_wgf;
+    uint8_t *const stage = reinterpret_cast<uint8_t *>(s_dyn);
+    uint32_t *const s_img = s_dyn + ((NB * SB) >> 2); // header image, 16 dwords per frame
+    uint32_t *const s_z = s_img + WF * 16;             // LCG state at the frame's first 16-B chunk
+    uint32_t *const s_a0 = s_z + WF;                   // lane 0's initial checksum accumulator
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t flags = K.flags;
+    const uint32_t flen = K.fixed_len, hl = K.hl;
+    const uint64_t f0 = (uint64_t)blockIdx.x * WF;
+    const uint64_t left = K.n_frames - f0;
+    const uint32_t nfr = left < WF ? (uint32_t)left : WF;
+    const uint64_t W0 = f0 * flen; // 16-B aligned
+
+    // lane constants: group grp builds frame w * NGW + grp of every window w
+    const uint32_t grp = tid / G, lg = tid % G;
+    const uint32_t r = grp * flen; // frame start, relative to its window
+    const uint32_t s0 = r & 15u;
+    const uint32_t ma = (s0 + hl) >> 4;           // first chunk holding payload
+    const uint32_t nch = (s0 + flen + 15u) >> 4;  // chunks the frame touches
+    const uint32_t e4 = ((s0 + flen) & 15u) >> 2; // dwords of the frame in its last chunk (0: all 4)
+    const uint32_t mlast = nch - 1u - lg;         // this lane's last chunk
+    const uint32_t cnt = mlast >= ma && mlast < nch ? (mlast - ma) / G + 1u : 0u;
+    const uint32_t mfirst = mlast - (cnt ? cnt - 1u : 0u) * G;
+    const uint2 Mm = K.lcg48[cnt ? mfirst : 0u];
+    const uint2 MG = K.lcg48[G];
+    const uint32_t mgy = pb_vgpr(MG.y);
+    const bool tail = lg == 0 && e4 != 0; // lane 0's final chunk is cut at dword e4
+
+    // ---------------- A: one lane per frame ----------------
+    const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
+    if (tid < nfr && !(K.fst_dbg & 8u))
+    {
+        const uint64_t f = f0 + tid;
+        const uint32_t hs0 = (((tid % NGW) * flen) & 15u) + hl;
+        const uint2 jt = K.jump[PB_JNEG - hs0];
+        const int j0 = (int)(16u * (hs0 >> 4)) - (int)hs0; // (-16, 0]: header bytes in chunk ma
+        const uint2 ja = K.jump[PB_JNEG + j0];
+        uint64_t k;
+        uint32_t pi;
+        pb_frame_index(K, f, k, pi);
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+        const uint32_t r0 = pb_rand_r(s);
+        const pb_frame_pl P = pb_payload(K, s, pi);
+        uint32_t d[16];
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
+        pb_u32x4 *row = reinterpret_cast<pb_u32x4 *>(s_img + tid * 16);
+        row[0] = pb_u32x4{d[0], d[1], d[2], d[3]};
+        row[1] = pb_u32x4{d[4], d[5], d[6], d[7]};
+        row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
+        row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
+        s_z[tid] = jt.x * P.st0 + jt.y;
+        if (L4)
+        {
+            uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) +
+                          pb_halves(d[12]) + pb_halves(d[13]);
+            if (flags & PBK_PSEUDO)
+                hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
+            // the generated header bytes of chunk ma, in output alignment (frames start on even bytes)
+            uint32_t gs = 0;
+            uint32_t x = ja.x * P.st0 + ja.y;
+            for (int p = 0; p < -j0; ++p)
+            {
+                gs += ((x >> 16) & 0xFFu) << (8 * (p & 1));
+                x = pb_step3(x, PB_A3, PB_C3);
+            }
+            // one's-complement arithmetic is mod 0xFFFF: add a multiple of it to stay >= 0
+            s_a0[tid] = hs + 16u * 0xFFFFu - gs;
+        }
+    }
+    __syncthreads();
+
+    const uint32_t nwin = (nfr + NGW - 1) / NGW;
+    const uint32_t hw = hl >> 2; // header dwords written whole; hl % 4 == 2: one more half dword
+    uint32_t sb = 0;
+    for (uint32_t w = 0; w < nwin; ++w)
+    {
+        uint8_t *const stg = stage + sb;
+        const uint32_t nfw = min(NGW, nfr - w * NGW);
+        const uint32_t fr = w * NGW + grp;
+        const bool live = grp < nfw;
+        // ---------------- B: payload chunks, then the group's header ----------------
+        uint32_t acc = 0;
+        if (live && cnt && !(K.fst_dbg & 1u))
+        {
+            if (L4 && lg == 0)
+                acc = s_a0[fr];
+            uint32_t x = __umul24(s_z[fr], Mm.x) + Mm.y;
+            pb_u32x4 *p = reinterpret_cast<pb_u32x4 *>(stg) + (r >> 4) + mfirst;
+            uint32_t o0, o1, o2, o3;
+            for (uint32_t i = 1; i < cnt; ++i)
+            {
+                pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+                if (L4)
+                    acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
+                *p = pb_u32x4{o0, o1, o2, o3};
+                p += G;
+                x = pb_mad24(x, MG.x, mgy);
+            }
+            // the lane's final chunk
+            pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+            if (tail)
+            {
+                uint32_t *q = reinterpret_cast<uint32_t *>(p);
+                o1 = e4 > 1u ? o1 : 0u;
+                o2 = e4 > 2u ? o2 : 0u;
+                o3 = 0u;
+                q[0] = o0;
+                if (e4 > 1u)
+                    q[1] = o1;
+                if (e4 > 2u)
+                    q[2] = o2;
+            }
+            else
+                *p = pb_u32x4{o0, o1, o2, o3};
+            if (L4)
+                acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
+        }
+        if (L4)
+            acc = pb_group_sum<G>(acc);
+        if (live && lg <= hw && !(K.fst_dbg & 1u))
+        {
+            uint32_t v = s_img[fr * 16 + lg];
+            if (L4)
+            {
+                const uint32_t c = (~pb_fold(acc)) & 0xFFFFu;
+                if (lg == K.csum_dw)
+                    v |= K.csum_hi ? (c << 16) : c;
+            }
+            uint32_t *hp = reinterpret_cast<uint32_t *>(stg + r) + lg;
+            if (lg < hw)
+                *hp = v;
+            else if (hl & 2u)
+                *reinterpret_cast<uint16_t *>(hp) = (uint16_t)v;
+        }
+        __syncthreads();
+
+        // ---------------- S: the window to HBM, contiguous 16-B stores ----------------
+        // window bytes [0, R1); a last chunk that is not whole (the launch's last,
+        // short window) is stored dword by dword.  Lane t stores the window's chunks
+        // whose absolute 16-B index is t mod 256, so each wave's store instruction
+        // covers one 1 KiB-aligned block and each step of the workgroup one 4 KiB
+        // page (wave stores straddling 1 KiB boundaries cost ~10% of the write
+        // rate: profiles/r01/wbench, shifted pages)
+        const uint32_t R1 = nfw * flen;
+        const uint32_t c1 = R1 >> 4;
+        const uint64_t gb = W0 + (uint64_t)w * NGW * flen;
+        uint8_t *const gout = K.out + gb;
+        const pb_u32x4 *const st16 = reinterpret_cast<const pb_u32x4 *>(stg);
+        uint32_t c = (K.fst_dbg & 2u) ? c1 : ((tid - (uint32_t)(gb >> 4)) & (PB_WG - 1u));
+        for (; c + 3 * PB_WG < c1; c += 4 * PB_WG)
+        {
+            const pb_u32x4 v0 = st16[c], v1 = st16[c + PB_WG], v2 = st16[c + 2 * PB_WG], v3 = st16[c + 3 * PB_WG];
+            pb_st16(gout + 16 * c, v0);
+            pb_st16(gout + 16 * (c + PB_WG), v1);
+            pb_st16(gout + 16 * (c + 2 * PB_WG), v2);
+            pb_st16(gout + 16 * (c + 3 * PB_WG), v3);
+        }
+        for (; c < c1; c += PB_WG)
+            pb_st16(gout + 16 * c, st16[c]);
+        if (tid == PB_WG - 1 && (R1 & 15u))
+        {
+            const uint32_t *sw = reinterpret_cast<const uint32_t *>(stg) + 4 * c1;
+            uint32_t *gw = reinterpret_cast<uint32_t *>(gout) + 4 * c1;
+            for (uint32_t t = 0; t < ((R1 & 15u) >> 2); ++t)
+                gw[t] = sw[t];
+        }
+        if (NB == 1)
+            __syncthreads(); // the next window reuses the stage
+        else
+            sb = sb ? 0u : SB;
+    }
+    if (blockIdx.x == 0 && tid == 0)
+    {
+        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
+        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+    }
+}
+
 // ---------------- variable length: lengths -> offsets -> tile map ----------------
 
 __global__ __launch_bounds__(256) void pb_len_reduce(pb_kargs K, unsigned long long *block_sums)
@@ -1574,7 +1798,28 @@ static void pbk_launch_small(const pb_kargs *K, uint32_t grid, hipStream_t st)
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid, hipStream_t st)
 {
-    if (K->gpf_g && !K->stage_win)
+    if (K->fst_g)
+    {
+        const uint32_t grid = (uint32_t)((K->n_frames + K->fst_wgf - 1) / K->fst_wgf);
+        const size_t lds = (size_t)K->fst_nbuf * K->fst_sb + PB_FST_LDS(K->fst_wgf);
+        const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
+#define PB_FST(GG)                                                                                    \
+    do                                                                                                \
+    {                                                                                                 \
+        if (l4)                                                                                       \
+            hipLaunchKernelGGL((pb_fstage_kernel<GG, true>), dim3(grid), dim3(PB_WG), lds, st, *K);  \
+        else                                                                                          \
+            hipLaunchKernelGGL((pb_fstage_kernel<GG, false>), dim3(grid), dim3(PB_WG), lds, st, *K); \
+    } while (0)
+        if (K->fst_g == 16)
+            PB_FST(16);
+        else if (K->fst_g == 32)
+            PB_FST(32);
+        else
+            PB_FST(64);
+#undef PB_FST
+    }
+    else if (K->gpf_g && !K->stage_win)
     {
         const uint32_t grid = (uint32_t)((K->n_frames + K->gpf_fpw - 1) / K->gpf_fpw);
         const uint32_t rm = K->gpf_rmode;

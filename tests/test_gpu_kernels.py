@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 
 SHAPES = [
     ("gpf", {"PBGPU_KERNEL": "gpf"}, ("pb_gpf_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
-    ("linear_small", {"PBGPU_KERNEL": "linear"}, ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel")),
+    ("linear_small", {"PBGPU_KERNEL": "linear"},
+     ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel")),
     ("tile", {"PBGPU_KERNEL": "tile"}, ("pb_build_kernel",)),
     ("stage_g8_wgf5", {"PBGPU_KERNEL": "stage", "PBGPU_G": "8", "PBGPU_WGF": "5"},
      ("pb_stage_kernel<8", "pb_xsmall_kernel", "pb_small_kernel<")),
@@ -27,6 +28,16 @@ SHAPES = [
      ("pb_stage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("stage_g32_kb36", {"PBGPU_KERNEL": "stage", "PBGPU_G": "32", "PBGPU_STAGE_KB": "36"},
      ("pb_stage_kernel<32", "pb_xsmall_kernel", "pb_small_kernel<")),
+]
+
+# pb_fstage_kernel shapes (fixed lengths > 128 B, multiple of 4, random payload)
+FST_SHAPES = [
+    ("fst_default", {}),
+    ("fst_g32", {"PBGPU_FST_G": "32"}),
+    ("fst_g16_nb2", {"PBGPU_FST_G": "16", "PBGPU_FST_NBUF": "2"}),
+    ("fst_g64_nb1", {"PBGPU_FST_G": "64", "PBGPU_FST_NBUF": "1"}),
+    ("fst_g16_nb1_wgf48", {"PBGPU_FST_G": "16", "PBGPU_FST_NBUF": "1", "PBGPU_FST_WGF": "48"}),
+    ("fst_g32_wgf256", {"PBGPU_FST_G": "32", "PBGPU_FST_WGF": "256"}),
 ]
 
 
@@ -115,3 +126,65 @@ def test_small_frames_pages(ctx, proto, flen):
         n = max(1, n * 64 // flen)  # page counts as named above at every length
         kern = _check(ctx, cfg, 1000003 + n, n)
         assert kern.startswith("pb_xsmall_kernel" if 4096 % flen == 0 else "pb_small_kernel<"), kern
+
+
+# pb_fstage_kernel: frame lengths (multiples of 4) that start frames at every
+# dword offset of a 16-B chunk and end them at every one, for each protocol,
+# with and without checksums; frame counts that leave a ragged last window and
+# a ragged last workgroup.
+FST_LENS = [132, 148, 256, 1000, 1500, 1508, 2052, 4096]
+FST_COUNTS = [1, 15, 17, 64, 65, 333, 1027]
+
+
+def _fst_cfg(proto, flen, csum=True):
+    hl = 54 if proto == "tcp" else 42
+    cfg = copy.deepcopy(pc.get({"udp": "c2_udp_1500", "tcp": "c4_tcp_syn", "icmp": "c5_icmp_echo"}[proto]))
+    cfg["payloads"] = [{"length": {"min": flen - hl, "max": flen - hl}}]
+    if not csum:
+        cfg["l4csum"] = 0
+    return cfg
+
+
+@pytest.mark.parametrize("shape,env", FST_SHAPES, ids=[s[0] for s in FST_SHAPES])
+@pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
+@pytest.mark.parametrize("flen", FST_LENS)
+def test_fstage_frames(ctx, monkeypatch, shape, env, proto, flen):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cfg = _fst_cfg(proto, flen)
+    for n in FST_COUNTS:
+        if n * flen > (8 << 20):
+            continue
+        kern = _check(ctx, cfg, 77 + 3 * n, n)
+        if _fst_fits(env, flen):
+            assert kern.startswith("pb_fstage_kernel<%s" % env.get("PBGPU_FST_G", "")), kern
+
+
+def _fst_fits(env, flen):
+    """Whether a forced shape fits 64 KiB of LDS (else the library takes pb_stage_kernel)."""
+    if "PBGPU_FST_G" not in env:
+        return True  # the default picks a shape that fits
+    g = int(env["PBGPU_FST_G"])
+    nbs = [int(env["PBGPU_FST_NBUF"])] if "PBGPU_FST_NBUF" in env else [1, 2]
+    ngw = 256 // g
+    wgf = max(ngw, min(256, int(env.get("PBGPU_FST_WGF", 64)) // ngw * ngw))
+    return any(nb * ((ngw * flen + 15) // 16 * 16) + wgf * 72 <= 65536 for nb in nbs)
+
+
+@pytest.mark.parametrize("flen", [132, 1500, 1508])
+def test_fstage_no_l4_csum(ctx, flen):
+    for proto in ("udp", "tcp", "icmp"):
+        cfg = _fst_cfg(proto, flen, csum=False)
+        kern = _check(ctx, cfg, 5, 1027)
+        assert kern.startswith("pb_fstage_kernel<") and kern.endswith(", 0>"), kern
+
+
+def test_fstage_not_for_other_shapes(ctx, monkeypatch):
+    """Lengths not a multiple of 4, static payloads and the literal rule keep
+    pb_stage_kernel; PBGPU_KERNEL=stage forces it."""
+    cfg = _fst_cfg("udp", 1502)
+    assert _check(ctx, cfg, 9, 100).startswith("pb_stage_kernel"), "odd dword"
+    cfg = _fst_cfg("udp", 1500)
+    assert _check(ctx, cfg, 9, 100, rule=1).startswith("pb_stage_kernel"), "literal rule"
+    monkeypatch.setenv("PBGPU_KERNEL", "stage")
+    assert _check(ctx, cfg, 9, 100).startswith("pb_stage_kernel"), "forced"
