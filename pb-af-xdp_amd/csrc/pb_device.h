@@ -118,11 +118,15 @@ struct pb_kargs
     uint32_t fst_wgf;       // frames per workgroup (a multiple of 256 / G, <= 256)
     uint32_t fst_sb;        // bytes per stage buffer (multiple of 16)
     uint32_t fst_nbuf;      // stage buffers: 2 (window w + 1 is built while w streams out) or 1
+    uint32_t vst;           // 1: the stage_* shape runs pb_vstage_kernel (every payload random, stream rule)
     uint32_t fst_dbg;       // diagnostics (PBGPU_FST_DBG, wrong output): bit 0 skips payload + headers,
                             // bit 1 the stores, bit 3 phase A (time decomposition)
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)
+// pb_vstage_kernel's LDS besides the stage: lcg48 entries, header image + start, length, z, header
+// sum, build order per frame, window list
+#define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + (size_t)(wgf) * (16 + 5) * 4 + ((size_t)(wgf) + 2) * 4)
 
 __device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)
 {

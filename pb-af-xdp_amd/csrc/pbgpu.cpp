@@ -766,7 +766,10 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             }
             else
             {
-                const uint32_t skb = ekb && atoi(ekb) > 0 ? (uint32_t)atoi(ekb) : 24;
+                // 24 KiB windows for pb_stage_kernel, 16 for pb_vstage_kernel (configs[2], 2^23
+                // frames: 1.74 ms at 16 KiB, 1.86 at 24, 2.40 at 36, 2.46 at 8; profiles/r01/vstage)
+                const bool vst_ok = K.gpf_rmode == 1 && !(flags & PBK_LITERAL) && !env_is("PBGPU_KERNEL", "stage");
+                const uint32_t skb = ekb && atoi(ekb) > 0 ? (uint32_t)atoi(ekb) : (vst_ok ? 16 : 24);
                 sbytes = (skb * 1024 + 15) / 16 * 16;
                 if (sbytes < 2 * maxf + 48)
                     sbytes = (2 * maxf + 48 + 15) / 16 * 16;
@@ -786,6 +789,15 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 K.stage_wgf = wgf;
                 K.stage_wgt = wgt;
                 K.stage_bytes = sbytes;
+                // every payload random, stream rule: pb_vstage_kernel (no header pass, no
+                // serial byte loops in phase A; configs[2] 1.74 vs 1.87 ms per 2^23 frames at
+                // the best window of each); PBGPU_KERNEL=stage keeps pb_stage_kernel
+                if (K.gpf_rmode == 1 && !(flags & PBK_LITERAL) && wgt == PB_WG && !env_is("PBGPU_KERNEL", "stage") &&
+                    sbytes + PB_VST_LDS(wgf) <= 64 * 1024)
+                {
+                    K.vst = 1;
+                    K.fst_dbg = (uint32_t)env_int("PBGPU_FST_DBG", 0);
+                }
             }
             // fixed-length staged kernel (pb_fstage_kernel): lengths > 128 B that are a
             // multiple of 4, every payload random, stream rule.  One stage buffer, then two;
@@ -1032,7 +1044,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     int rc = timed_pair(ctx, &tp);
     if (rc)
         return rc;
-    const bool timing = K.stage_win && !K.fst_g && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
+    const bool timing = K.stage_win && !K.fst_g && !K.vst && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
     const uint64_t n_wg = K.stage_wgf ? (nf + K.stage_wgf - 1) / K.stage_wgf : 0;
     if (timing)
     {
@@ -1326,6 +1338,8 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
     const pb_kargs &K = S.K;
     if (K.fst_g)
         snprintf(buf, n, "pb_fstage_kernel<%u, %u>", K.fst_g, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
+    else if (K.stage_win && K.vst)
+        snprintf(buf, n, "pb_vstage_kernel<%u, %u>", K.gpf_g, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
     else if (K.stage_win)
         snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.gpf_g)

@@ -1598,6 +1598,296 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
     }
 }
 
+// ---------------- any length, every payload random: pb_vstage_kernel ----------------
+//
+// Packed variable-length frames (configs[2]) and fixed lengths that are not a
+// multiple of 4: pb_stage_kernel's windows (frames starting in bytes
+// [w W, (w + 1) W) of the workgroup's output), with the per-frame work cut:
+//  * the stage is zero before a window is built (S zeroes what it streamed), so
+//    a chunk two frames share (a frame's last chunk = the next frame's first) is
+//    assembled with LDS ORs of each frame's own bytes, in any order; every other
+//    chunk belongs to one frame and is a plain 16-B write;
+//  * the group writes its frame's header itself once its checksum is known (the
+//    header image shifted to the frame's byte offset, ORed into the chunks it
+//    shares with the payload / the previous frame): no header pass and no
+//    barrier between payload and headers;
+//  * the first payload chunk's header bytes and the last chunk's bytes past the
+//    frame are masked in the payload loop, so phase A has no serial byte loops.
+// Lane lg of a group takes chunks nch-1-lg, nch-1-lg-G, ... as in pb_fstage_kernel.
+template <int G, bool L4>
+__global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
+{
+    constexpr uint32_t NGW = PB_WG / G; // frames in flight per workgroup
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    const uint32_t WF = K.stage_wgf, W = K.stage_win, SB = K.stage_bytes;
+    pb_u32x4 *const stage = reinterpret_cast<pb_u32x4 *>(s_dyn);
+    uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_dyn + (SB >> 2)); // lcg48[0 .. PB_STAGE_L48)
+    uint32_t *const s_img = s_dyn + (SB >> 2) + 2 * PB_STAGE_L48;      // header image, 16 dwords per frame
+    uint32_t *const s_r = s_img + WF * 16;                             // frame start, workgroup-relative
+    uint32_t *const s_len = s_r + WF;
+    uint32_t *const s_z = s_len + WF;  // LCG state at the frame's first 16-B chunk
+    uint32_t *const s_hs = s_z + WF;   // header + pseudo header word sum, folded (frame alignment)
+    uint32_t *const s_win = s_hs + WF; // s_win[w]: first frame of window w, [nwin] = nfr
+    uint32_t *const s_ord = s_win + WF + 2; // frames of each window, longest first
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t flags = K.flags;
+    const uint32_t hl = K.hl;
+    const uint64_t f0 = (uint64_t)blockIdx.x * WF;
+    const uint64_t left = K.n_frames - f0;
+    const uint32_t nfr = left < WF ? (uint32_t)left : WF;
+    const uint64_t W0 = K.fixed_len ? f0 * K.fixed_len : K.offsets[f0];
+    const uint64_t wbase = W0 & ~15ull;
+    const uint32_t nsc = SB >> 4; // stage chunks
+
+    // ---------------- A: one lane per frame; the stage starts zero ----------------
+    uint2 l48v[(PB_STAGE_L48 + PB_WG - 1) / PB_WG];
+#pragma unroll
+    for (uint32_t i = 0; i < (PB_STAGE_L48 + PB_WG - 1) / PB_WG; ++i)
+        if (tid + i * PB_WG < PB_STAGE_L48)
+            l48v[i] = K.lcg48[tid + i * PB_WG];
+    for (uint32_t c = tid; c < nsc; c += PB_WG)
+        stage[c] = pb_u32x4{0u, 0u, 0u, 0u};
+    uint32_t my_r = 0;
+    const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
+    if (tid < nfr)
+    {
+        const uint64_t f = f0 + tid;
+        uint64_t base;
+        uint32_t flen;
+        if (K.fixed_len)
+        {
+            base = f * K.fixed_len;
+            flen = K.fixed_len;
+        }
+        else
+        {
+            base = K.offsets[f];
+            flen = (uint32_t)(K.offsets[f + 1] - base);
+        }
+        my_r = (uint32_t)(base - wbase);
+        // state at payload index -((r % 16) + hl): the first byte of the frame's first chunk
+        const uint2 jt = K.jump[PB_JNEG - ((my_r & 15u) + hl)];
+        uint64_t k;
+        uint32_t pi;
+        pb_frame_index(K, f, k, pi);
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+        const uint32_t r0 = pb_rand_r(s);
+        const pb_frame_pl P = pb_payload(K, s, pi);
+        uint32_t d[16];
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
+        pb_u32x4 *row = reinterpret_cast<pb_u32x4 *>(s_img + tid * 16);
+        row[0] = pb_u32x4{d[0], d[1], d[2], d[3]};
+        row[1] = pb_u32x4{d[4], d[5], d[6], d[7]};
+        row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
+        row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
+        s_r[tid] = my_r;
+        s_len[tid] = flen;
+        s_z[tid] = jt.x * P.st0 + jt.y;
+        if (L4)
+        {
+            uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) +
+                          pb_halves(d[12]) + pb_halves(d[13]);
+            if (flags & PBK_PSEUDO)
+                hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
+            s_hs[tid] = pb_fold(hs);
+        }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < (PB_STAGE_L48 + PB_WG - 1) / PB_WG; ++i)
+        if (tid + i * PB_WG < PB_STAGE_L48)
+            s_l48[tid + i * PB_WG] = l48v[i];
+    __syncthreads();
+    // window starts: frame t opens windows (r_{t-1} / W, r_t / W]  (W >= the longest frame)
+    if (tid < nfr)
+    {
+        const uint32_t w = my_r / W;
+        const uint32_t wp = tid ? s_r[tid - 1] / W : 0u;
+        if (tid == 0)
+            s_win[0] = 0;
+        for (uint32_t v = wp + 1; v <= w; ++v)
+            s_win[v] = tid;
+        if (tid == nfr - 1)
+            s_win[w + 1] = nfr;
+    }
+    __syncthreads();
+    const uint32_t nwin = s_r[nfr - 1] / W + 1;
+    // the frames of a window ordered longest first, so a wave's groups build frames of
+    // similar length (random lengths: the wave runs as long as its longest frame);
+    // windows of more than 64 frames keep their order
+    if (tid < nfr)
+    {
+        const uint32_t w = my_r / W;
+        const uint32_t b = s_win[w], e = s_win[w + 1];
+        uint32_t rank = tid - b;
+        if (e - b <= 64)
+        {
+            const uint32_t len = s_len[tid];
+            rank = 0;
+            for (uint32_t u = b; u < e; ++u)
+            {
+                const uint32_t lu = s_len[u];
+                rank += (lu > len || (lu == len && u < tid)) ? 1u : 0u;
+            }
+        }
+        s_ord[b + rank] = tid;
+    }
+    __syncthreads();
+
+    const uint32_t grp = tid / G, lg = tid % G;
+    const uint2 MG = s_l48[G];
+    const uint32_t mgy = pb_vgpr(MG.y);
+    for (uint32_t w = 0; w < nwin; ++w)
+    {
+        const uint32_t sb = s_win[w], se = s_win[w + 1];
+        const uint32_t R0 = s_r[sb]; // window bytes [R0, R1), workgroup-relative
+        const uint32_t R1 = s_r[se - 1] + s_len[se - 1];
+        const uint32_t sbase = R0 & ~15u;
+
+        // ---------------- B: G lanes per frame, payload chunks, then the header ----------------
+        for (uint32_t k = sb + grp; k < (K.fst_dbg & 1u ? sb : se); k += NGW)
+        {
+            const uint32_t fr = s_ord[k];
+            const uint32_t r = s_r[fr] - sbase;
+            const uint32_t s0 = r & 15u, cf = r >> 4;
+            const uint32_t hend = s0 + hl;                   // header end, frame-chunk relative
+            const uint32_t fend = s0 + s_len[fr];            // frame end
+            const uint32_t ma = hend >> 4;                   // first chunk holding payload
+            const uint32_t nch = (fend + 15u) >> 4;          // chunks the frame touches
+            const uint32_t mlast = nch - 1u - lg;            // this lane's last chunk (wraps if none)
+            const uint32_t cnt = mlast < nch && mlast >= ma ? (mlast - ma) / G + 1u : 0u;
+            uint32_t acc = 0;
+            if (cnt)
+            {
+                // edge chunks (the lane's first may be chunk ma, lane 0's last the frame's last)
+                // are masked in the first and last passes only; the passes between are plain
+                uint32_t m = mlast - (cnt - 1u) * G;
+                const uint2 Mm = s_l48[m];
+                uint32_t x = __umul24(s_z[fr], Mm.x) + Mm.y;
+                pb_u32x4 *p = stage + cf + m;
+                auto edge = [&](uint32_t mm, pb_u32x4 *pp) {
+                    uint32_t o0, o1, o2, o3;
+                    pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+                    const bool last = mm + 1u == nch;
+                    const int lo = mm == ma ? (int)(hend & 15u) : 0;
+                    const int hi = last ? (int)(fend - 16u * mm) : 16;
+                    if (lo > 0 || hi < 16)
+                    {
+                        o0 &= pb_range_mask(lo, hi);
+                        o1 &= pb_range_mask(lo - 4, hi - 4);
+                        o2 &= pb_range_mask(lo - 8, hi - 8);
+                        o3 &= pb_range_mask(lo - 12, hi - 12);
+                    }
+                    if (L4)
+                        acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
+                    if (hi < 16) // shared with the next frame
+                    {
+                        uint32_t *q = reinterpret_cast<uint32_t *>(pp);
+                        atomicOr(q + 0, o0);
+                        atomicOr(q + 1, o1);
+                        atomicOr(q + 2, o2);
+                        atomicOr(q + 3, o3);
+                    }
+                    else
+                        *pp = pb_u32x4{o0, o1, o2, o3};
+                };
+                edge(m, p);
+                for (uint32_t i = 2; i < cnt; ++i)
+                {
+                    x = pb_mad24(x, MG.x, mgy);
+                    m += G;
+                    p += G;
+                    uint32_t o0, o1, o2, o3;
+                    pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+                    if (L4)
+                        acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
+                    *p = pb_u32x4{o0, o1, o2, o3};
+                }
+                if (cnt > 1u)
+                {
+                    x = pb_mad24(x, MG.x, mgy);
+                    m += G;
+                    p += G;
+                    edge(m, p);
+                }
+            }
+            uint32_t *const img = s_img + fr * 16;
+            if (L4)
+            {
+                acc = pb_group_sum<G>(acc);
+                if (lg == 0)
+                {
+                    // chunk sums were taken in output alignment
+                    uint32_t pc = pb_fold(acc);
+                    if (r & 1u)
+                        pc = pb_bswap16(pc);
+                    const uint32_t c = (~pb_fold(s_hs[fr] + pc)) & 0xFFFFu;
+                    img[K.csum_dw] |= K.csum_hi ? (c << 16) : c;
+                }
+            }
+            // header chunks 0 .. nhc-1: the image shifted to byte s0 (the image is zero past hl);
+            // the first is shared with the previous frame unless s0 == 0, the last with the
+            // payload (or the next frame) unless the header ends on the chunk edge
+            const uint32_t nhc = (hend + 15u) >> 4;
+            if (lg < nhc)
+            {
+                uint32_t h[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                {
+                    const int xb = (int)(16u * lg) - (int)s0 + 4 * t;
+                    const int i0 = xb >> 2;
+                    const uint32_t lo = (i0 >= 0 && i0 < 16) ? img[i0] : 0u;
+                    const uint32_t hi = (i0 + 1 >= 0 && i0 + 1 < 16) ? img[i0 + 1] : 0u;
+                    h[t] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)xb & 3u);
+                }
+                pb_u32x4 *p = stage + cf + lg;
+                if ((lg == 0 && s0) || (lg + 1u == nhc && (hend & 15u)))
+                {
+                    uint32_t *q = reinterpret_cast<uint32_t *>(p);
+                    atomicOr(q + 0, h[0]);
+                    atomicOr(q + 1, h[1]);
+                    atomicOr(q + 2, h[2]);
+                    atomicOr(q + 3, h[3]);
+                }
+                else
+                    *p = pb_u32x4{h[0], h[1], h[2], h[3]};
+            }
+        }
+        __syncthreads();
+
+        // ---------------- S: stage -> HBM, contiguous 16-B stores, then zero ----------------
+        // chunks [c0, c1) whole; 0 (lo_b != 0) and c1 (hi_b % 16 != 0) are shared with the
+        // neighbouring windows and byte-masked, each by the lane that then zeroes it
+        const uint32_t lo_b = R0 - sbase, hi_b = R1 - sbase;
+        const uint32_t c0 = lo_b ? 1u : 0u, c1 = hi_b >> 4;
+        uint8_t *const gout = K.out + wbase + sbase;
+        if (tid == 0 && lo_b)
+        {
+            const pb_u32x4 v = stage[0];
+            pb_store_chunk(gout, v[0], v[1], v[2], v[3], -(int)lo_b, (int)(hi_b - lo_b));
+        }
+        if ((hi_b & 15u) && tid == (c1 & (PB_WG - 1u)))
+        {
+            const pb_u32x4 v = stage[c1];
+            pb_store_chunk(gout + 16 * c1, v[0], v[1], v[2], v[3], (int)(16 * c1) - (int)lo_b,
+                           (int)(hi_b - lo_b));
+        }
+        for (uint32_t c = tid; c < nsc; c += PB_WG)
+        {
+            if (c >= c0 && c < c1 && !(K.fst_dbg & 2u))
+                pb_st16(gout + 16 * c, stage[c]);
+            stage[c] = pb_u32x4{0u, 0u, 0u, 0u};
+        }
+        __syncthreads(); // the next window reuses the (zeroed) stage
+    }
+    if (K.fixed_len && blockIdx.x == 0 && tid == 0)
+    {
+        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
+        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+    }
+}
+
 // ---------------- variable length: lengths -> offsets -> tile map ----------------
 
 __global__ __launch_bounds__(256) void pb_len_reduce(pb_kargs K, unsigned long long *block_sums)
@@ -1849,6 +2139,29 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid,
         }
 #undef PB_GPF_RM
 #undef PB_GPF
+    }
+    else if (K->stage_win && K->vst)
+    {
+        const uint32_t grid = (uint32_t)((K->n_frames + K->stage_wgf - 1) / K->stage_wgf);
+        const size_t lds = K->stage_bytes + PB_VST_LDS(K->stage_wgf);
+        const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
+#define PB_VST(GG)                                                                                    \
+    do                                                                                                \
+    {                                                                                                 \
+        if (l4)                                                                                       \
+            hipLaunchKernelGGL((pb_vstage_kernel<GG, true>), dim3(grid), dim3(PB_WG), lds, st, *K);  \
+        else                                                                                          \
+            hipLaunchKernelGGL((pb_vstage_kernel<GG, false>), dim3(grid), dim3(PB_WG), lds, st, *K); \
+    } while (0)
+        if (K->gpf_g == 8)
+            PB_VST(8);
+        else if (K->gpf_g == 16)
+            PB_VST(16);
+        else if (K->gpf_g == 32)
+            PB_VST(32);
+        else
+            PB_VST(64);
+#undef PB_VST
     }
     else if (K->stage_win)
     {

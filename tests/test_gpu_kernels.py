@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 SHAPES = [
     ("gpf", {"PBGPU_KERNEL": "gpf"}, ("pb_gpf_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("linear_small", {"PBGPU_KERNEL": "linear"},
-     ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel")),
+     ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel")),
     ("tile", {"PBGPU_KERNEL": "tile"}, ("pb_build_kernel",)),
     ("stage_g8_wgf5", {"PBGPU_KERNEL": "stage", "PBGPU_G": "8", "PBGPU_WGF": "5"},
      ("pb_stage_kernel<8", "pb_xsmall_kernel", "pb_small_kernel<")),
@@ -28,6 +28,14 @@ SHAPES = [
      ("pb_stage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("stage_g32_kb36", {"PBGPU_KERNEL": "stage", "PBGPU_G": "32", "PBGPU_STAGE_KB": "36"},
      ("pb_stage_kernel<32", "pb_xsmall_kernel", "pb_small_kernel<")),
+    # pb_vstage_kernel (random payloads) at other lane-group / window / workgroup sizes;
+    # static and mixed payloads keep pb_stage_kernel at the same shape
+    ("vstage_g16", {"PBGPU_G": "16"},
+     ("pb_vstage_kernel<16", "pb_stage_kernel<16", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
+    ("vstage_g64_kb8", {"PBGPU_G": "64", "PBGPU_STAGE_KB": "8"},
+     ("pb_vstage_kernel<64", "pb_stage_kernel<64", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
+    ("vstage_g32_wgf7", {"PBGPU_G": "32", "PBGPU_WGF": "7"},
+     ("pb_vstage_kernel<32", "pb_stage_kernel<32", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
 ]
 
 # pb_fstage_kernel shapes (fixed lengths > 128 B, multiple of 4, random payload)
@@ -96,7 +104,7 @@ def test_huge_frames(ctx, plen):
     cfg = copy.deepcopy(pc.get("c2_udp_1500"))
     cfg["payloads"] = [{"length": {"min": plen, "max": plen}}]
     kern = _check(ctx, cfg, 7, 96)
-    assert kern.startswith("pb_stage_kernel" if plen < 58000 else "pb_gpf_kernel"), kern
+    assert kern.startswith(("pb_vstage_kernel", "pb_stage_kernel") if plen < 58000 else "pb_gpf_kernel"), kern
     cfg["payloads"] = [{"length": {"min": 30000, "max": plen}}]
     kern = _check(ctx, cfg, 7, 96)
     assert kern.startswith("pb_gpf_kernel"), kern
@@ -180,11 +188,39 @@ def test_fstage_no_l4_csum(ctx, flen):
 
 
 def test_fstage_not_for_other_shapes(ctx, monkeypatch):
-    """Lengths not a multiple of 4, static payloads and the literal rule keep
+    """Lengths not a multiple of 4 take pb_vstage_kernel, the literal rule keeps
     pb_stage_kernel; PBGPU_KERNEL=stage forces it."""
     cfg = _fst_cfg("udp", 1502)
-    assert _check(ctx, cfg, 9, 100).startswith("pb_stage_kernel"), "odd dword"
+    assert _check(ctx, cfg, 9, 100).startswith("pb_vstage_kernel"), "odd dword"
     cfg = _fst_cfg("udp", 1500)
     assert _check(ctx, cfg, 9, 100, rule=1).startswith("pb_stage_kernel"), "literal rule"
     monkeypatch.setenv("PBGPU_KERNEL", "stage")
     assert _check(ctx, cfg, 9, 100).startswith("pb_stage_kernel"), "forced"
+
+
+# pb_vstage_kernel on fixed lengths that are not a multiple of 4 (frames start at
+# every byte offset of a chunk), with and without L4 checksums
+VST_LENS = [129, 130, 131, 133, 1501, 1502, 1503, 4097]
+
+
+@pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
+@pytest.mark.parametrize("flen", VST_LENS)
+def test_vstage_fixed_odd_lengths(ctx, proto, flen):
+    for csum in (True, False):
+        cfg = _fst_cfg(proto, flen, csum)
+        for n in (1, 7, 33, 129, 1031):
+            kern = _check(ctx, cfg, 3 + n, n)
+            assert kern.startswith("pb_vstage_kernel<"), kern
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 1), (0, 5), (0, 40), (60, 1500), (1400, 1500), (0, 3000)])
+@pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
+def test_vstage_variable_lengths(ctx, proto, lo, hi):
+    """Packed variable frames from header-only (frames sharing chunks on both
+    sides, empty payloads) to 3 KB."""
+    hl = 54 if proto == "tcp" else 42
+    cfg = _fst_cfg(proto, hl + 100)
+    cfg["payloads"] = [{"length": {"min": lo, "max": hi}}]
+    n = max(64, min(6000, (6 << 20) // (hl + hi + 1)))
+    kern = _check(ctx, cfg, 11, n)
+    assert kern.startswith("pb_vstage_kernel<"), kern
