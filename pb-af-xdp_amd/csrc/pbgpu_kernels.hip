@@ -52,35 +52,15 @@ __device__ __forceinline__ uint32_t pb_jump(const pb_kargs &K, uint32_t s, uint3
     return t.x * s + t.y;
 }
 
-// Payload i of an iteration whose seed is s (sequence.c:529-561).
-__device__ __forceinline__ pb_frame_pl pb_payload(const pb_kargs &K, uint32_t s, uint32_t i)
+// One payload's draw from the seed state `cur` entering it (sequence.c:529-561).
+__device__ __forceinline__ pb_frame_pl pb_payload_of(const pb_pl &P, uint32_t cur, uint32_t flags)
 {
-    pb_pl P;
-    uint32_t cur = s;
-    if (K.pl_cnt == 1)
-    {
-        P = K.pl0;
-    }
-    else
-    {
-        // earlier random payloads advance the seed by one rand_r per byte
-        for (uint32_t p = 0; p < i; ++p)
-        {
-            const pb_pl Q = K.pls[p];
-            if (Q.random)
-            {
-                const uint32_t len = Q.min_len + pb_mod(pb_rand_r(cur), Q.len);
-                cur = pb_jump(K, cur, len);
-            }
-        }
-        P = K.pls[i];
-    }
     pb_frame_pl r;
     if (P.random)
     {
         r.random = 1;
         r.plen = P.min_len + pb_mod(pb_rand_r(cur), P.len);
-        r.nvalid = (K.flags & PBK_LITERAL) ? min(r.plen, 1u) : r.plen;
+        r.nvalid = (flags & PBK_LITERAL) ? min(r.plen, 1u) : r.plen;
         r.st0 = cur;
         r.blob_off = 0;
         r.ssum = 0;
@@ -95,6 +75,28 @@ __device__ __forceinline__ pb_frame_pl pb_payload(const pb_kargs &K, uint32_t s,
         r.ssum = P.ssum;
     }
     return r;
+}
+
+// Payload i of an iteration whose seed is s (sequence.c:529-561).  The payload
+// record is read in place (kernel argument or device table): a local copy chosen
+// from either became a stack object, 16 B of scratch stores per lane per
+// workgroup (~4% of the staged kernels' HBM writes, PMC WRITE_SIZE).
+__device__ __forceinline__ pb_frame_pl pb_payload(const pb_kargs &K, uint32_t s, uint32_t i)
+{
+    if (K.pl_cnt == 1)
+        return pb_payload_of(K.pl0, s, K.flags);
+    // earlier random payloads advance the seed by one rand_r per byte
+    uint32_t cur = s;
+    for (uint32_t p = 0; p < i; ++p)
+    {
+        const pb_pl &Q = K.pls[p];
+        if (Q.random)
+        {
+            const uint32_t len = Q.min_len + pb_mod(pb_rand_r(cur), Q.len);
+            cur = pb_jump(K, cur, len);
+        }
+    }
+    return pb_payload_of(K.pls[i], cur, K.flags);
 }
 
 __device__ __forceinline__ void pb_frame_index(const pb_kargs &K, uint64_t f, uint64_t &k, uint32_t &i)
