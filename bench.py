@@ -87,6 +87,9 @@ def run_config(ctx, name, seq_idx, n_pkts, steps, warmup, rank, world, dist, loc
     seq = Sequence.from_config(pc.get(name))
     ctx.load_sequence(seq_idx, seq, pc.SEED_BASE)
     fb = ctx.alloc_frames(*ctx.build_size(seq_idx, n_pkts))
+    # span timing: one HIP-event pair around the timed launches, none per launch
+    # (a per-launch pair writes back the L2 twice per launch: ~9 us gaps)
+    ctx.set_timing(ctx.TIMING_SPAN)
     step_iter = lambda s: pb_dist.step_first_iter(s, rank, world, n_pkts)  # noqa: E731
     t_ramp = time.perf_counter()
     while time.perf_counter() - t_ramp < ramp_s:

@@ -123,8 +123,18 @@ int pbgpu_host_unregister(pbgpu_ctx *ctx, void *ptr);
 int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq);
 
 /* ---- measurement ---- */
-/* Device time of the frame-build kernels launched since the last call:
- * sum over launches (ms) and launch count (HIP events on the ctx stream). */
+/* Device time of the frame-build kernels launched since the last call, from
+ * HIP events on the ctx stream, and the launch count.  PBGPU_TIMING_LAUNCH
+ * (default): an event pair around every launch, ms_total = the sum of the
+ * kernels' durations.  PBGPU_TIMING_SPAN: one event before the first launch
+ * after the last call and one at this call, ms_total = the span on the device
+ * (launch gaps included).  Each timing event is a release to system scope that
+ * writes back the L2's dirty lines: the per-launch pair costs ~9 us between
+ * back-to-back 2-GiB launches, so a continuously sending caller
+ * runs in span mode. */
+#define PBGPU_TIMING_LAUNCH 0
+#define PBGPU_TIMING_SPAN 1
+int pbgpu_set_timing(pbgpu_ctx *ctx, int mode);
 int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches);
 /* Write-only roofline probe: `reps` launches of each of three 16-B/lane fill
  * shapes over `bytes` (16 KiB per workgroup plain / non-temporal, 4 KiB per

@@ -101,6 +101,9 @@ struct pbgpu_ctx
     seq_slot seqs[PB_MAX_SEQUENCES];
     std::vector<timing_pair> pending;
     std::vector<timing_pair> pool;
+    int timing_mode = PBGPU_TIMING_LAUNCH;
+    timing_pair span = {nullptr, nullptr}; // PBGPU_TIMING_SPAN: first-launch / call events
+    uint32_t span_n = 0;                    // launches in the open span (0: none open)
     uint8_t *h_stage = nullptr;
     uint16_t *d_lens = nullptr; // copy_to_umem: frame lengths of the mapped scatter (device)
     uint16_t *h_lens = nullptr; // ... and their pinned host copy
@@ -384,6 +387,11 @@ void pbgpu_close(pbgpu_ctx *ctx)
     {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
+    }
+    if (ctx->span.a)
+    {
+        (void)hipEventDestroy(ctx->span.a);
+        (void)hipEventDestroy(ctx->span.b);
     }
     if (ctx->d_jump)
         (void)hipFree(ctx->d_jump);
@@ -1040,9 +1048,10 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             K.xs_grid = K.xs_full + (uint32_t)((nch - (uint64_t)K.xs_full * np + np - 1) / np);
         }
     }
-    timing_pair tp;
-    int rc = timed_pair(ctx, &tp);
-    if (rc)
+    const bool span = ctx->timing_mode == PBGPU_TIMING_SPAN;
+    timing_pair tp = {nullptr, nullptr};
+    int rc = PBGPU_OK;
+    if (!span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
         return rc;
     const bool timing = K.stage_win && !K.fst_g && !K.vst && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
     const uint64_t n_wg = K.stage_wgf ? (nf + K.stage_wgf - 1) / K.stage_wgf : 0;
@@ -1058,6 +1067,21 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         }
         HIPCHK(hipMemsetAsync(ctx->d_dbg, 0, n_wg * 8 * sizeof(unsigned long long), ctx->stream));
         K.dbg = ctx->d_dbg;
+    }
+    if (span)
+    {
+        if (ctx->span_n == 0)
+        {
+            if (ctx->span.a == nullptr)
+            {
+                HIPCHK(hipEventCreate(&ctx->span.a));
+                HIPCHK(hipEventCreate(&ctx->span.b));
+            }
+            HIPCHK(hipEventRecord(ctx->span.a, ctx->stream));
+        }
+        HIPCHK(pbk_launch_build(&K, (uint32_t)n_tiles, ctx->stream));
+        ++ctx->span_n;
+        return PBGPU_OK;
     }
     HIPCHK(hipEventRecord(tp.a, ctx->stream));
     HIPCHK(pbk_launch_build(&K, (uint32_t)n_tiles, ctx->stream));
@@ -1263,6 +1287,19 @@ int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)
     return bad ? PBGPU_EIO : PBGPU_OK;
 }
 
+int pbgpu_set_timing(pbgpu_ctx *ctx, int mode)
+{
+    if (ctx == NULL || (mode != PBGPU_TIMING_LAUNCH && mode != PBGPU_TIMING_SPAN))
+        return PBGPU_EINVAL;
+    double ms; // close what the old mode measured
+    uint32_t n;
+    const int rc = pbgpu_kernel_time(ctx, &ms, &n);
+    if (rc)
+        return rc;
+    ctx->timing_mode = mode;
+    return PBGPU_OK;
+}
+
 int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches)
 {
     if (ctx == NULL)
@@ -1270,6 +1307,16 @@ int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches)
     HIPCHK(hipSetDevice(ctx->device));
     double tot = 0;
     uint32_t n = 0;
+    if (ctx->span_n)
+    {
+        HIPCHK(hipEventRecord(ctx->span.b, ctx->stream));
+        HIPCHK(hipEventSynchronize(ctx->span.b));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ctx->span.a, ctx->span.b));
+        tot += ms;
+        n += ctx->span_n;
+        ctx->span_n = 0;
+    }
     for (auto &p : ctx->pending)
     {
         HIPCHK(hipEventSynchronize(p.b));

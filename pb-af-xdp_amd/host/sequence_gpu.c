@@ -103,6 +103,8 @@ static void *gpu_worker(void *p)
         last_error = rc;
         goto out;
     }
+    /* a continuous sender never reads per-launch timings: no event pair per batch */
+    (void)pbgpu_set_timing(ctx, PBGPU_TIMING_SPAN);
     pb_rules_t rules = {w->cmd.literal_payload ? PB_PAYLOAD_LITERAL : PB_PAYLOAD_STREAM,
                         w->cmd.single_fold ? PB_FOLD_SINGLE : PB_FOLD_FULL};
     /* MACs: a zero source MAC is the device's, a zero destination MAC the default

@@ -282,6 +282,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pbgpu_host_unregister": (C.c_int, [P, P]),
         "pbgpu_counters": (C.c_int, [P, U64P, U64P, C.c_int]),
         "pbgpu_kernel_time": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
+        "pbgpu_set_timing": (C.c_int, [P, C.c_int]),
         "pbgpu_fill_probe": (C.c_int, [P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
         "pbgpu_tile_bytes": (C.c_int, [P, C.c_uint16, C.POINTER(C.c_uint32)]),
         "pbgpu_abi_size": (C.c_size_t, [C.c_int]),
@@ -405,6 +406,13 @@ class GpuContext:
         _check(self.lib.pbgpu_counters(self.h, p.ctypes.data_as(C.POINTER(C.c_uint64)),
                                        b.ctypes.data_as(C.POINTER(C.c_uint64)), n_seq), "counters")
         return p, b
+
+    TIMING_LAUNCH, TIMING_SPAN = 0, 1
+
+    def set_timing(self, mode: int) -> None:
+        """PBGPU_TIMING_LAUNCH: an event pair per launch; PBGPU_TIMING_SPAN: one
+        span per kernel_time() call (no per-launch events)."""
+        _check(self.lib.pbgpu_set_timing(self.h, mode), "set_timing")
 
     def kernel_time(self):
         ms, n = C.c_double(), C.c_uint32()

@@ -241,3 +241,26 @@ def test_fill_probe_runs(ctx):
     ms = ctx.fill_probe(1 << 30, 5)
     gbps = (1 << 30) / (ms * 1e-3) / 1e9
     assert 500 < gbps < 9000
+
+
+def test_timing_modes(ctx):
+    """PBGPU_TIMING_LAUNCH sums per-launch event pairs; PBGPU_TIMING_SPAN spans
+    the launches since the last kernel_time() with one pair; output identical."""
+    seq = Sequence.from_config(pc.get("c2_udp_1500"))
+    ctx.load_sequence(0, seq, pc.SEED_BASE)
+    n = 4096
+    fb = ctx.alloc_frames(*ctx.build_size(0, n))
+    out = {}
+    for mode in (ctx.TIMING_SPAN, ctx.TIMING_LAUNCH):
+        ctx.set_timing(mode)
+        for s in range(3):
+            ctx.build(0, 1000 + s * n, n, fb)
+        ctx.sync()
+        ms, k = ctx.kernel_time()
+        assert k == 3 and ms > 0
+        assert ctx.kernel_time() == (0.0, 0)
+        out[mode] = fb.packed().copy()
+    assert np.array_equal(out[0], out[1])
+    with pytest.raises(pbgpu.PbError):
+        ctx.set_timing(7)
+    fb.free()
