@@ -1833,16 +1833,23 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             const uint32_t nhc = (hend + 15u) >> 4;
             if (lg < nhc)
             {
+                // frame bytes [16 lg - s0, 16 lg - s0 + 16): image dwords i0 .. i0 + 4, those
+                // outside the 16-dword row (a neighbour's image or another LDS array; never
+                // outside the allocation) read as zero
+                const int xb = (int)(16u * lg) - (int)s0;
+                const int i0 = xb >> 2;
+                const uint32_t sh = (uint32_t)xb & 3u;
+                uint32_t wv[5];
+#pragma unroll
+                for (int t = 0; t < 5; ++t)
+                {
+                    const uint32_t v = img[i0 + t];
+                    wv[t] = (uint32_t)(i0 + t) < 16u ? v : 0u;
+                }
                 uint32_t h[4];
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
-                {
-                    const int xb = (int)(16u * lg) - (int)s0 + 4 * t;
-                    const int i0 = xb >> 2;
-                    const uint32_t lo = (i0 >= 0 && i0 < 16) ? img[i0] : 0u;
-                    const uint32_t hi = (i0 + 1 >= 0 && i0 + 1 < 16) ? img[i0 + 1] : 0u;
-                    h[t] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)xb & 3u);
-                }
+                    h[t] = __builtin_amdgcn_alignbyte(wv[t + 1], wv[t], sh);
                 pb_u32x4 *p = stage + cf + lg;
                 if ((lg == 0 && s0) || (lg + 1u == nhc && (hend & 15u)))
                 {
