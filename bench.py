@@ -215,6 +215,7 @@ def main():
             "kernel": v["kernel"], "kernel_ms_avg": round(v["kernel_ms_avg"], 4),
             "roofline_achieved_gbps": round(ach15, 1), "roofline_frac": round(ach15 / HBM_PEAK_GBPS, 4),
             "frac_of_guide_achievable": round(ach15 / HBM_ACHIEVABLE_GBPS, 4),
+            "traffic": pmc_traffic(a.pmc, "c2_udp_1500"), "algorithmic_bytes_per_launch": v["bytes_per_launch"],
             "packets_per_launch": a.packets}
         if rank == 0:
             extra["d2h_umem_64B"] = d2h_rate(ctx, 0, a.packets)
