@@ -224,3 +224,19 @@ def test_vstage_variable_lengths(ctx, proto, lo, hi):
     n = max(64, min(6000, (6 << 20) // (hl + hi + 1)))
     kern = _check(ctx, cfg, 11, n)
     assert kern.startswith("pb_vstage_kernel<"), kern
+
+
+@pytest.mark.parametrize("pls", [
+    [{"length": {"min": 10, "max": 50}}, {"length": {"min": 100, "max": 200}}],
+    [{"length": {"min": 1458, "max": 1458}}, {"length": {"min": 1458, "max": 1458}}],
+    [{"length": {"min": 0, "max": 3}}, {"length": {"min": 7, "max": 7}}, {"length": {"min": 500, "max": 1400}}],
+], ids=["two_var", "two_fixed_1500", "three_mixed_lengths"])
+@pytest.mark.parametrize("proto", ["udp", "tcp"])
+def test_multi_random_payloads(ctx, proto, pls):
+    """Several random payloads per iteration (one frame each, later payloads drawn
+    from the advanced seed, sequence.c:529-561): packed variable frames through
+    pb_vstage_kernel, bit-exact against the oracle."""
+    cfg = _fst_cfg(proto, 200)
+    cfg["payloads"] = pls
+    kern = _check(ctx, cfg, 31, 1500)
+    assert kern.startswith("pb_vstage_kernel<"), kern
