@@ -144,10 +144,12 @@ def d2h_rate(ctx, seq_idx, n_pkts):
         ctx.build(seq_idx, r * n, n, fb)
         fb.to_umem(umem, 4096, 0, n)
     dt = (time.perf_counter() - t0) / reps
+    frame_bytes = fb.total_bytes()
     fb.free()
     ctx.kernel_time()
     ctx.lib.pbgpu_host_unregister(ctx.h, umem.ctypes.data)
-    return {"packets": n, "mpps": n / dt / 1e6, "ms_per_batch": dt * 1e3, "slot": 4096}
+    return {"packets": n, "mpps": n / dt / 1e6, "ms_per_batch": dt * 1e3, "slot": 4096,
+            "frame_gbps": frame_bytes / dt / 1e9}
 
 
 def cpu_baseline(name, budget_s, threads=None, faithful=True):
@@ -219,6 +221,7 @@ def main():
             "packets_per_launch": a.packets}
         if rank == 0:
             extra["d2h_umem_64B"] = d2h_rate(ctx, 0, a.packets)
+            extra["d2h_umem_1500B"] = d2h_rate(ctx, 1, a.packets)
     ctx.close()
     if rank != 0:
         return
