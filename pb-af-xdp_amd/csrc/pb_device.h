@@ -22,6 +22,9 @@
 #define PB_STAGE_L48 72                    // lcg48 entries the staged kernel keeps in LDS (> 4 + 64)
 #define PB_STAGE_LDS(wgf) ((size_t)(wgf) * (16 + 8) * 4 + 4 + PB_STAGE_L48 * 8) // its LDS besides the stage
 #define PB_LCG48_N 4200                    // lcg48[m] = L^(48 m), m < 4200 (> 16-B chunks of a 64 KiB frame)
+#define PB_XPG 4096                        // XCD-owned page bytes (pb_xsmall_kernel, pb_xpage_kernel)
+#define PB_XREG (PB_XPG + 256)             // LDS bytes per page region (128 B slack either side)
+#define PB_XNP_MAX 8                       // pb_xsmall_kernel: pages per workgroup, 4 (64-B frames) or 8 (128-B)
 
 // glibc LCG
 #define PB_LCG_A 1103515245u
@@ -112,6 +115,11 @@ struct pb_kargs
     uint32_t xs_nch;        // pages of this launch's stream
     uint32_t xs_full;       // workgroups [0, xs_full) own XCD-strided pages; the rest take the tail pages in order
     uint32_t xs_grid;       // >0: launch pb_xsmall_kernel with this many workgroups
+    // pb_xpage_kernel (the xs_* page shape for lengths % 4 == 0 that do not divide 4096)
+    uint32_t xp;            // 1: use it
+    uint32_t xp_fpp;        // frame slots per page: the most frames touching one page
+    pb_div xp_div;          // division by xp_fpp
+    double xp_inv;          // 1.0 / flen
     // fixed-length staged kernel (pb_fstage_kernel): frame length a multiple of 4, every
     // payload random, stream rule; one frame per G-lane group per window of 256 / G frames
     uint32_t fst_g;         // >0: launch it with G lanes per frame (16, 32, 64)

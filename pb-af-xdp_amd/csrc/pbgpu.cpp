@@ -665,11 +665,31 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     if (fixed && pls.size() == 1 && minf <= 128)
     {
         K.small_ndw = minf <= 64 ? 16 : 32;
-        if (4096 % minf == 0) // pages of whole frames: pb_xsmall_kernel
+        const bool xp_force = env_is("PBGPU_XP_FORCE", "1"); // experiments: pb_xpage_kernel for any length % 4 == 0
+        if (4096 % minf == 0 && !xp_force) // pages of whole frames: pb_xsmall_kernel
         {
             while ((minf << K.xs_fp_shift) < 4096)
                 ++K.xs_fp_shift;
             K.xs_np = 256 >> K.xs_fp_shift;
+        }
+        else if (minf % 4 == 0 && ((K.proto == 6 && minf <= 64) || xp_force) && !env_is("PBGPU_KERNEL", "nopage"))
+        {
+            // pages of frames cut at the page edges (pb_xpage_kernel): one slot per frame
+            // touching a page; pages per workgroup = the slots of two passes of 256 lanes,
+            // at most 7 (30 KiB of LDS, 5 workgroups per CU).  60-B TCP SYN, 2^25 frames
+            // (profiles/r01/xpage): 7 pages 0.318-0.336 ms, 4 / 3 / 2 pages 0.387 / 0.405 /
+            // 0.50, 10 / 14 pages 0.374 / 0.458; the linear small kernel 0.353-0.372.  Taken
+            // for TCP frames <= 64 B only: by length and protocol (len_ab.txt) it ties for
+            // 60-B UDP and loses 12-20% for 44-48-B UDP and every frame over 64 B
+            // (PBGPU_XP_FORCE=1 takes it for any length % 4 == 0).
+            K.xp = 1;
+            K.xp_fpp = (4096 + minf - 1) / minf + 1;
+            K.xp_div = make_div(K.xp_fpp);
+            K.xp_inv = 1.0 / (double)minf;
+            K.xs_np = std::max<uint32_t>(1, std::min<uint32_t>(7, 2 * PB_WG / K.xp_fpp));
+            const int enp = env_int("PBGPU_XP_NP", 0);
+            if (enp > 0 && (size_t)enp * PB_XREG <= 64 * 1024)
+                K.xs_np = (uint32_t)enp;
         }
         if (!pls[0].random)
         {
@@ -1393,7 +1413,8 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.small_ndw)
         snprintf(buf, n, "%s<%u, %u, %s>",
-                 K.xs_np && !env_is("PBGPU_KERNEL", "linear") ? "pb_xsmall_kernel" : "pb_small_kernel",
+                 K.xs_np && !env_is("PBGPU_KERNEL", "linear") ? (K.xp ? "pb_xpage_kernel" : "pb_xsmall_kernel")
+                                                               : "pb_small_kernel",
                  K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
     else
         snprintf(buf, n, "pb_build_kernel<%s>", K.fixed_len ? "true" : "false");

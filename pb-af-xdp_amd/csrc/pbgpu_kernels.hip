@@ -727,9 +727,6 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
 // Lengths that do not divide 4096 cut frames at page edges; building those
 // frames in both owners measured slower than the linear form (60-B TCP 0.37 vs
 // 0.345 ms, 98-B ICMP 0.70 vs 0.64), so they keep pb_small_kernel.
-#define PB_XPG 4096                  // page bytes
-#define PB_XREG (PB_XPG + 256)       // LDS bytes per page region (128 B slack either side)
-#define PB_XNP_MAX 8                 // pages per workgroup: 4 (64-B frames) or 8 (128-B)
 
 template <int NDW, int PROTO, bool RANDOM>
 __global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
@@ -769,6 +766,78 @@ __global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
         {
             const uint32_t sl = (i * PB_XREG + 128) / 16 + tid;
             pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[pb_swz(sl)];
+            if (o + 16 > T) // last chunk of the stream: zero the tail
+            {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
+            }
+            pb_st16(K.out + o, v);
+        }
+    }
+    if (b == 0 && tid == 0)
+    {
+        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
+        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+    }
+}
+
+// XCD-owned pages for frame lengths that are a multiple of 4 but do not divide
+// 4096 (60-B TCP SYN, configs[3]): pb_xsmall_kernel's page ownership, with the
+// frames that straddle a page edge built by both owners.  Slot j of page i is
+// frame floor(4096 c_i / flen) + j (found per lane with a double reciprocal and a
+// +-1 fix-up: no prologue, no barrier before the build); the frame is written
+// whole into the page's LDS region, whose 128 B of slack either side take the
+// bytes outside the page and are never stored.  At 60 B one frame in 69 is built
+// twice.
+template <int NDW, int PROTO, bool RANDOM>
+__global__ __launch_bounds__(PB_WG) void pb_xpage_kernel(pb_kargs K)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[]; // K.xs_np page regions
+    const uint32_t tid = threadIdx.x, b = blockIdx.x;
+    const uint32_t flen = K.fixed_len;
+    const uint32_t np = K.xs_np, fpp = K.xp_fpp;
+    const uint64_t T = K.total_bytes;
+    uint32_t c0, cs;
+    if (b < K.xs_full)
+        c0 = (b >> 3) * (np * 8) + (b & 7u), cs = 8;
+    else
+        c0 = K.xs_full * np + (b - K.xs_full) * np, cs = 1;
+
+    for (uint32_t sl = tid; sl < np * fpp; sl += PB_WG)
+    {
+        const uint32_t i = pb_divq(sl, K.xp_div), j = sl - i * fpp;
+        const uint32_t c = c0 + i * cs;
+        if (c >= K.xs_nch)
+            continue;
+        const uint64_t p0 = (uint64_t)c * PB_XPG;
+        uint64_t fa = (uint64_t)((double)p0 * K.xp_inv); // floor(p0 / flen), +-1
+        if (fa * flen > p0)
+            --fa;
+        else if ((fa + 1) * flen <= p0)
+            ++fa;
+        const uint64_t f = fa + j;
+        if (f >= K.n_frames || f * flen >= p0 + PB_XPG)
+            continue;
+        uint32_t d[NDW];
+        pb_small_frame<NDW, PROTO, RANDOM>(K, f, d);
+        const int off = (int)((int64_t)(f * flen) - (int64_t)p0); // (-flen, 4096), dword aligned
+        uint32_t *row = s_tile + (i * PB_XREG + 128 + off) / 4;
+#pragma unroll
+        for (int t = 0; t < NDW; ++t)
+            if ((uint32_t)(4 * t) < flen)
+                row[t] = d[t];
+    }
+    __syncthreads();
+
+    // page i -> HBM: one 16-B store per lane per page
+    for (uint32_t i = 0; i < np; ++i)
+    {
+        const uint32_t c = c0 + i * cs;
+        const uint64_t o = (uint64_t)c * PB_XPG + 16 * tid;
+        if (c < K.xs_nch && o < T)
+        {
+            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[(i * PB_XREG + 128) / 16 + tid];
             if (o + 16 > T) // last chunk of the stream: zero the tail
             {
 #pragma unroll
@@ -2068,7 +2137,15 @@ __global__ __launch_bounds__(256) void pb_fill_kernel(pb_u32x4 *dst, uint64_t n1
 template <int NDW, int PROTO>
 static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
 {
-    if (K->pl0.random)
+    if (K->xs_grid && K->xp)
+    {
+        const size_t lds = (size_t)K->xs_np * PB_XREG;
+        if (K->pl0.random)
+            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), lds, st, *K);
+        else
+            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false>), dim3(K->xs_grid), dim3(PB_WG), lds, st, *K);
+    }
+    else if (K->pl0.random)
     {
         if (K->xs_grid)
             hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), 0, st, *K);

@@ -5,6 +5,7 @@ and the tile kernel, each bit-exact against the CPU oracle on every config.
 Selection is through the library's PBGPU_* environment overrides, which
 pbgpu_load_sequence() reads.  Run on the MI355X box: pytest -m gpu."""
 import copy
+import os
 
 import numpy as np
 import pytest
@@ -17,6 +18,11 @@ pytestmark = pytest.mark.gpu
 
 SHAPES = [
     ("gpf", {"PBGPU_KERNEL": "gpf"}, ("pb_gpf_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
+    ("nopage_small", {"PBGPU_KERNEL": "nopage"},
+     ("pb_small_kernel", "pb_xsmall_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel")),
+    ("xpage_forced", {"PBGPU_XP_FORCE": "1"},
+     ("pb_xpage_kernel", "pb_xsmall_kernel", "pb_small_kernel<", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel",
+      "pb_vstage_kernel")),
     ("linear_small", {"PBGPU_KERNEL": "linear"},
      ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel")),
     ("tile", {"PBGPU_KERNEL": "tile"}, ("pb_build_kernel",)),
@@ -85,6 +91,8 @@ def test_kernel_shape_matches_oracle(ctx, monkeypatch, shape, env, kernels, name
         monkeypatch.setenv(k, v)
     cfg = pc.get(name)
     kern = _check(ctx, cfg, 123456789, _iters(cfg))
+    if "pb_xsmall_kernel" in kernels:  # small frames keep their page kernels under the staged overrides
+        kernels = kernels + ("pb_xpage_kernel",)
     assert kern.startswith(kernels), kern
 
 
@@ -111,17 +119,21 @@ def test_huge_frames(ctx, plen):
 
 
 # Small frames: lengths dividing 4096 (64, 128 B) take pb_xsmall_kernel (4 KiB
-# pages owned per XCD), the others pb_small_kernel.  Frame lengths 42..128 B
+# pages owned per XCD), other multiples of 4 pb_xpage_kernel (the same pages, frames
+# cut at page edges built by both owners), the rest pb_small_kernel.  Frame lengths 42..128 B
 # cover every LDS placement mode (16-B, 8-B, 4-B and byte-aligned frames); the
 # frame counts hit < 1 page, exactly 32 pages (one full group of 8 workgroups),
 # one frame past it, and a ragged tail after several full groups.
-XS_LENS = [42, 43, 60, 64, 72, 96, 98, 106, 127, 128]
+XS_LENS = [42, 43, 44, 48, 60, 64, 72, 96, 98, 100, 106, 108, 116, 120, 124, 127, 128]
 XS_COUNTS = [1, 5, 200, 2048, 2049, 2 * 2048 * 5 + 77]
 
 
+@pytest.mark.parametrize("force_xpage", [False, True], ids=["default", "xpage_forced"])
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
 @pytest.mark.parametrize("flen", XS_LENS)
-def test_small_frames_pages(ctx, proto, flen):
+def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
+    if force_xpage:
+        monkeypatch.setenv("PBGPU_XP_FORCE", "1")
     hl = 54 if proto == "tcp" else 42
     if flen < hl or (proto == "icmp" and flen == hl):
         pytest.skip("shorter than the headers / empty static payload")
@@ -133,7 +145,11 @@ def test_small_frames_pages(ctx, proto, flen):
     for n in XS_COUNTS:
         n = max(1, n * 64 // flen)  # page counts as named above at every length
         kern = _check(ctx, cfg, 1000003 + n, n)
-        assert kern.startswith("pb_xsmall_kernel" if 4096 % flen == 0 else "pb_small_kernel<"), kern
+        if flen % 4 == 0 and (force_xpage or (4096 % flen and proto == "tcp" and flen <= 64)):
+            want = "pb_xpage_kernel"
+        else:
+            want = "pb_xsmall_kernel" if 4096 % flen == 0 else "pb_small_kernel<"
+        assert kern.startswith(want), kern
 
 
 # pb_fstage_kernel: frame lengths (multiples of 4) that start frames at every
