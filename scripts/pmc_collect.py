@@ -23,7 +23,7 @@ for d in sorted(glob.glob(os.path.join(out_dir, "pmc_*"))):
         agg = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"]
-            if not (kn.startswith("void pb_") and ("gpf" in kn or "stage" in kn or "small" in kn or "build_kernel" in kn)):
+            if not (kn.startswith("void pb_") and ("gpf" in kn or "stage" in kn or "small" in kn or "xpage" in kn or "build_kernel" in kn)):
                 continue
             agg[(kn, r["Counter_Name"])].append(float(r["Counter_Value"]))
         for (kn, cn), v in agg.items():
