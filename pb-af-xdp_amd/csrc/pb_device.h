@@ -120,6 +120,7 @@ struct pb_kargs
     uint32_t xp_fpp;        // frame slots per page: the most frames touching one page
     pb_div xp_div;          // division by xp_fpp
     double xp_inv;          // 1.0 / flen
+    uint32_t xp_wgt;        // threads per workgroup: 256 (two slots per lane) or 512 (one)
     // fixed-length staged kernel (pb_fstage_kernel): frame length a multiple of 4, every
     // payload random, stream rule; one frame per G-lane group per window of 256 / G frames
     uint32_t fst_g;         // >0: launch it with G lanes per frame (16, 32, 64)

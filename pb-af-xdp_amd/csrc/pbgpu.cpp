@@ -687,8 +687,9 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             K.xp_div = make_div(K.xp_fpp);
             K.xp_inv = 1.0 / (double)minf;
             K.xs_np = std::max<uint32_t>(1, std::min<uint32_t>(7, 2 * PB_WG / K.xp_fpp));
-            const int enp = env_int("PBGPU_XP_NP", 0);
-            if (enp > 0 && (size_t)enp * PB_XREG <= 64 * 1024)
+            K.xp_wgt = (uint32_t)env_int("PBGPU_XP_WGT", 256) == 512 ? 512 : 256;
+            const int enp = env_int("PBGPU_XP_NP", 0); // at most two frame slots per 256 lanes
+            if (enp > 0 && (uint32_t)enp * K.xp_fpp <= 2 * PB_WG)
                 K.xs_np = (uint32_t)enp;
         }
         if (!pls[0].random)

@@ -790,8 +790,8 @@ __global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
 // whole into the page's LDS region, whose 128 B of slack either side take the
 // bytes outside the page and are never stored.  At 60 B one frame in 69 is built
 // twice.
-template <int NDW, int PROTO, bool RANDOM>
-__global__ __launch_bounds__(PB_WG) void pb_xpage_kernel(pb_kargs K)
+template <int NDW, int PROTO, bool RANDOM, int WGT>
+__global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[]; // K.xs_np page regions
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
@@ -804,8 +804,16 @@ __global__ __launch_bounds__(PB_WG) void pb_xpage_kernel(pb_kargs K)
     else
         c0 = K.xs_full * np + (b - K.xs_full) * np, cs = 1;
 
-    for (uint32_t sl = tid; sl < np * fpp; sl += PB_WG)
+    // at most two slots per 256 lanes (np * fpp <= 512): one straight-line pass per
+    // 512-thread workgroup, two unrolled passes per 256-thread one (a loop kept the
+    // kernel arguments live across iterations and spilled them through v_readlane /
+    // v_writelane, 41 VALU per frame)
+#pragma unroll
+    for (uint32_t pass = 0; pass < 512 / WGT; ++pass)
     {
+        const uint32_t sl = tid + pass * WGT;
+        if (sl >= np * fpp)
+            break;
         const uint32_t i = pb_divq(sl, K.xp_div), j = sl - i * fpp;
         const uint32_t c = c0 + i * cs;
         if (c >= K.xs_nch)
@@ -830,14 +838,15 @@ __global__ __launch_bounds__(PB_WG) void pb_xpage_kernel(pb_kargs K)
     }
     __syncthreads();
 
-    // page i -> HBM: one 16-B store per lane per page
-    for (uint32_t i = 0; i < np; ++i)
+    // page i -> HBM: one 16-B store per lane per page (256 lanes per page)
+    for (uint32_t i = tid / 256; i < np; i += WGT / 256)
     {
+        const uint32_t l = tid % 256;
         const uint32_t c = c0 + i * cs;
-        const uint64_t o = (uint64_t)c * PB_XPG + 16 * tid;
+        const uint64_t o = (uint64_t)c * PB_XPG + 16 * l;
         if (c < K.xs_nch && o < T)
         {
-            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[(i * PB_XREG + 128) / 16 + tid];
+            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[(i * PB_XREG + 128) / 16 + l];
             if (o + 16 > T) // last chunk of the stream: zero the tail
             {
 #pragma unroll
@@ -2140,10 +2149,15 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
     if (K->xs_grid && K->xp)
     {
         const size_t lds = (size_t)K->xs_np * PB_XREG;
-        if (K->pl0.random)
-            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), lds, st, *K);
+        const bool w512 = K->xp_wgt == 512;
+        if (K->pl0.random && w512)
+            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, 512>), dim3(K->xs_grid), dim3(512), lds, st, *K);
+        else if (K->pl0.random)
+            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, PB_WG>), dim3(K->xs_grid), dim3(PB_WG), lds, st, *K);
+        else if (w512)
+            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false, 512>), dim3(K->xs_grid), dim3(512), lds, st, *K);
         else
-            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false>), dim3(K->xs_grid), dim3(PB_WG), lds, st, *K);
+            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false, PB_WG>), dim3(K->xs_grid), dim3(PB_WG), lds, st, *K);
     }
     else if (K->pl0.random)
     {

@@ -128,12 +128,14 @@ XS_LENS = [42, 43, 44, 48, 60, 64, 72, 96, 98, 100, 106, 108, 116, 120, 124, 127
 XS_COUNTS = [1, 5, 200, 2048, 2049, 2 * 2048 * 5 + 77]
 
 
-@pytest.mark.parametrize("force_xpage", [False, True], ids=["default", "xpage_forced"])
+@pytest.mark.parametrize("force_xpage", [False, True, 512], ids=["default", "xpage_forced", "xpage_forced_512"])
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
 @pytest.mark.parametrize("flen", XS_LENS)
 def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
     if force_xpage:
         monkeypatch.setenv("PBGPU_XP_FORCE", "1")
+    if force_xpage == 512:
+        monkeypatch.setenv("PBGPU_XP_WGT", "512")
     hl = 54 if proto == "tcp" else 42
     if flen < hl or (proto == "icmp" and flen == hl):
         pytest.skip("shorter than the headers / empty static payload")
