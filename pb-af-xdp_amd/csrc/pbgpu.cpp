@@ -672,16 +672,18 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 ++K.xs_fp_shift;
             K.xs_np = 256 >> K.xs_fp_shift;
         }
-        else if (minf % 4 == 0 && ((K.proto == 6 && minf <= 64) || xp_force) && !env_is("PBGPU_KERNEL", "nopage"))
+        else if (minf % 4 == 0 && ((minf <= 64 && 2 * PB_WG / ((4096 + minf - 1) / minf + 1) >= 6) || xp_force) &&
+                 !env_is("PBGPU_KERNEL", "nopage"))
         {
             // pages of frames cut at the page edges (pb_xpage_kernel): one slot per frame
             // touching a page; pages per workgroup = the slots of two passes of 256 lanes,
             // at most 7 (30 KiB of LDS, 5 workgroups per CU).  60-B TCP SYN, 2^25 frames
             // (profiles/r01/xpage): 7 pages 0.318-0.336 ms, 4 / 3 / 2 pages 0.387 / 0.405 /
             // 0.50, 10 / 14 pages 0.374 / 0.458; the linear small kernel 0.353-0.372.  Taken
-            // for TCP frames <= 64 B only: by length and protocol (len_ab.txt) it ties for
-            // 60-B UDP and loses 12-20% for 44-48-B UDP and every frame over 64 B
-            // (PBGPU_XP_FORCE=1 takes it for any length % 4 == 0).
+            // for frames <= 64 B whose workgroup gets >= 6 pages (52-64 B): by length
+            // (len_ab.txt) it wins 4-12% there for UDP and TCP, loses 5-12% at 44-48 B (5
+            // pages) and 12-20% over 64 B, where the 32-dword frame spills kernel-argument
+            // SGPRs (PBGPU_XP_FORCE=1 takes it for any length % 4 == 0).
             K.xp = 1;
             K.xp_fpp = (4096 + minf - 1) / minf + 1;
             K.xp_div = make_div(K.xp_fpp);

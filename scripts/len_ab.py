@@ -1,4 +1,5 @@
-"""pb_xpage_kernel vs the linear small kernel over frame lengths (UDP, random payload), in process."""
+"""pb_xpage_kernel (forced) vs the linear small kernel over frame lengths, in process.
+python3 len_ab.py [udp|small]"""
 import copy
 import json
 import os
@@ -16,6 +17,8 @@ CASES = [(p, f, r) for p, f, r in (
     ("tcp", 60, 4), ("tcp", 60, 1), ("tcp", 72, 4), ("tcp", 100, 4), ("tcp", 120, 4))]
 if len(sys.argv) > 1 and sys.argv[1] == "udp":
     CASES = [("udp", f, 1) for f in (44, 48, 60, 72, 100, 120, 124)]
+if len(sys.argv) > 1 and sys.argv[1] == "small":
+    CASES = [("udp", f, 1) for f in (44, 48, 52, 56, 60)] + [("udp", 60, 4), ("tcp", 56, 4), ("tcp", 60, 4)]
 for proto, flen, nr in CASES:
     cfg = copy.deepcopy(pc.get("c4_tcp_syn" if proto == "tcp" else "c2_udp_64"))
     hl = 54 if proto == "tcp" else 42
@@ -27,8 +30,10 @@ for proto, flen, nr in CASES:
         for tag, env in (("xpage", None), ("linear", "nopage")):
             if env:
                 os.environ["PBGPU_KERNEL"] = env
+                os.environ.pop("PBGPU_XP_FORCE", None)
             else:
                 os.environ.pop("PBGPU_KERNEL", None)
+                os.environ["PBGPU_XP_FORCE"] = "1"
             ctx.load_sequence(0, Sequence.from_config(cfg), pc.SEED_BASE)
             fb = ctx.alloc_frames(*ctx.build_size(0, n))
             for s in range(3):

@@ -124,7 +124,7 @@ def test_huge_frames(ctx, plen):
 # cover every LDS placement mode (16-B, 8-B, 4-B and byte-aligned frames); the
 # frame counts hit < 1 page, exactly 32 pages (one full group of 8 workgroups),
 # one frame past it, and a ragged tail after several full groups.
-XS_LENS = [42, 43, 44, 48, 60, 64, 72, 96, 98, 100, 106, 108, 116, 120, 124, 127, 128]
+XS_LENS = [42, 43, 44, 48, 52, 56, 60, 64, 72, 96, 98, 100, 106, 108, 116, 120, 124, 127, 128]
 XS_COUNTS = [1, 5, 200, 2048, 2049, 2 * 2048 * 5 + 77]
 
 
@@ -147,7 +147,8 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
     for n in XS_COUNTS:
         n = max(1, n * 64 // flen)  # page counts as named above at every length
         kern = _check(ctx, cfg, 1000003 + n, n)
-        if flen % 4 == 0 and (force_xpage or (4096 % flen and proto == "tcp" and flen <= 64)):
+        xp_default = flen <= 64 and 512 // ((4096 + flen - 1) // flen + 1) >= 6
+        if flen % 4 == 0 and (force_xpage or (4096 % flen and xp_default)):
             want = "pb_xpage_kernel"
         else:
             want = "pb_xsmall_kernel" if 4096 % flen == 0 else "pb_small_kernel<"
