@@ -129,7 +129,8 @@ struct pb_kargs
     uint32_t fst_nbuf;      // stage buffers: 2 (window w + 1 is built while w streams out) or 1
     uint32_t vst;           // 1: the stage_* shape runs pb_vstage_kernel (every payload random, stream rule)
     uint32_t fst_dbg;       // diagnostics (PBGPU_FST_DBG, wrong output): bit 0 skips payload + headers,
-                            // bit 1 the stores, bit 3 phase A (time decomposition)
+                            // bit 1 the stores, bit 3 phase A (time decomposition);
+                            // pb_vstage_kernel: bit 4 fixed 8-lane groups, bit 5 no 32-lane groups (A/B)
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

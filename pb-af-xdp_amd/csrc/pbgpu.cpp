@@ -811,7 +811,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 const uint32_t fw = win / maxf; // whole windows per workgroup
                 wgf = fw > wgt ? wgt : std::min<uint32_t>(wgt / fw * fw, fw * ((wgf + fw - 1) / fw));
             }
-            else
+            else if (!getenv("PBGPU_WGF"))
                 wgf = std::min<uint32_t>(wgt, std::max(wgf, win / minf + 1));
             if (!gpf_only && sbytes + PB_STAGE_LDS(wgf) <= 64 * 1024)
             {

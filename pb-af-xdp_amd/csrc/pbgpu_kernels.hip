@@ -165,6 +165,14 @@ __device__ __forceinline__ uint32_t pb_mad24(uint32_t x, uint32_t a, uint32_t c)
 }
 
 // a uniform value held in a VGPR (one v_mov outside the loops that use it)
+// the same with a per-lane multiplier (lanes of one wave in groups of different sizes)
+__device__ __forceinline__ uint32_t pb_mad24v(uint32_t x, uint32_t a, uint32_t c)
+{
+    uint32_t r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(a), "v"(c));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t pb_vgpr(uint32_t s)
 {
     uint32_t v;
@@ -1814,9 +1822,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     }
     __syncthreads();
 
-    const uint32_t grp = tid / G, lg = tid % G;
-    const uint2 MG = s_l48[G];
-    const uint32_t mgy = pb_vgpr(MG.y);
     for (uint32_t w = 0; w < nwin; ++w)
     {
         const uint32_t sb = s_win[w], se = s_win[w + 1];
@@ -1824,8 +1829,32 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         const uint32_t R1 = s_r[se - 1] + s_len[se - 1];
         const uint32_t sbase = R0 & ~15u;
 
-        // ---------------- B: G lanes per frame, payload chunks, then the header ----------------
-        for (uint32_t k = sb + grp; k < (K.fst_dbg & 1u ? sb : se); k += NGW)
+        // lanes per frame: G, or (G = 8, windows of F <= 32 frames) every lane busy — the
+        // window's longest frames (s_ord is longest first) take 32 / 16 lanes: y frames of
+        // 32, then x of 16, then 8 each, groups aligned to their size
+        uint32_t g = G, grp0 = tid / G, lg = tid % G;
+        if (G == 8 && !(K.fst_dbg & 16u))
+        {
+            const uint32_t F = se - sb;
+            uint32_t y = 0, x = 0;
+            if (F <= 16u)
+            {
+                y = K.fst_dbg & 32u ? 0u : (F <= 8u ? F : 16u - F);
+                x = F - y;
+            }
+            else if (F <= 32u)
+                x = 32u - F;
+            if (tid < 32u * y)
+                g = 32, grp0 = tid >> 5, lg = tid & 31u;
+            else if (tid < 32u * y + 16u * x)
+                g = 16, grp0 = y + ((tid - 32u * y) >> 4), lg = tid & 15u;
+            else
+                grp0 = y + x + ((tid - 32u * y - 16u * x) >> 3), lg = tid & 7u;
+        }
+        const uint2 MG = s_l48[g];
+
+        // ---------------- B: g lanes per frame, payload chunks, then the header ----------------
+        for (uint32_t k = sb + grp0; k < (K.fst_dbg & 1u ? sb : se); k += NGW)
         {
             const uint32_t fr = s_ord[k];
             const uint32_t r = s_r[fr] - sbase;
@@ -1835,13 +1864,13 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             const uint32_t ma = hend >> 4;                   // first chunk holding payload
             const uint32_t nch = (fend + 15u) >> 4;          // chunks the frame touches
             const uint32_t mlast = nch - 1u - lg;            // this lane's last chunk (wraps if none)
-            const uint32_t cnt = mlast < nch && mlast >= ma ? (mlast - ma) / G + 1u : 0u;
+            const uint32_t cnt = mlast < nch && mlast >= ma ? (mlast - ma) / g + 1u : 0u;
             uint32_t acc = 0;
             if (cnt)
             {
                 // edge chunks (the lane's first may be chunk ma, lane 0's last the frame's last)
                 // are masked in the first and last passes only; the passes between are plain
-                uint32_t m = mlast - (cnt - 1u) * G;
+                uint32_t m = mlast - (cnt - 1u) * g;
                 const uint2 Mm = s_l48[m];
                 uint32_t x = __umul24(s_z[fr], Mm.x) + Mm.y;
                 pb_u32x4 *p = stage + cf + m;
@@ -1874,9 +1903,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                 edge(m, p);
                 for (uint32_t i = 2; i < cnt; ++i)
                 {
-                    x = pb_mad24(x, MG.x, mgy);
-                    m += G;
-                    p += G;
+                    x = pb_mad24v(x, MG.x, MG.y);
+                    m += g;
+                    p += g;
                     uint32_t o0, o1, o2, o3;
                     pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
                     if (L4)
@@ -1885,16 +1914,25 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                 }
                 if (cnt > 1u)
                 {
-                    x = pb_mad24(x, MG.x, mgy);
-                    m += G;
-                    p += G;
+                    x = pb_mad24v(x, MG.x, MG.y);
+                    m += g;
+                    p += g;
                     edge(m, p);
                 }
             }
             uint32_t *const img = s_img + fr * 16;
             if (L4)
             {
-                acc = pb_group_sum<G>(acc);
+                if (G == 8)
+                {
+                    // sums over 8, 16 and 32 lanes; each lane keeps its own group's
+                    const uint32_t a8 = pb_group_sum<8>(acc);
+                    const uint32_t a16 = a8 + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a8, 0x128, 0xF, 0xF, false);
+                    const uint32_t a32 = a16 + __shfl_xor(a16, 16, 64);
+                    acc = g == 8 ? a8 : (g == 16 ? a16 : a32);
+                }
+                else
+                    acc = pb_group_sum<G>(acc);
                 if (lg == 0)
                 {
                     // chunk sums were taken in output alignment
