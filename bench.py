@@ -3,20 +3,27 @@
 BASELINE.json metric: "device-resident Mpps & GB/s, 64B and 1500B UDP, L3+L4
 checksums on".  One step = one launch building 2^25 packets of configs[1]
 (UDP 64-B frame, random /16 source + source port, 22-B random payload, both
-checksums) into HBM.  Multi-GPU: one process per GPU, each
-rank builds its own disjoint iteration range (weak scaling, no data-path
-collective); the global packet / byte counters are all-reduced over RCCL once
-at the end of the timed region (the reference's total_pckts/total_bytes,
-sequence.c:12-14).
+checksums) into HBM.  --config picks another BASELINE
+workload for the same line shape: c2_udp_1500, c3_udp_var (configs[2]),
+c4_tcp_syn (configs[3]) and c5_mix (configs[4]: three sequences — UDP 64 B, TCP
+SYN 60 B, ICMP 98 B — built per step, 2^24 iterations each per GPU).
+
+Multi-GPU: one process per GPU, each rank builds its own disjoint iteration
+range (weak scaling, no data-path collective).  The only exchange is the
+reference's global counter (total_pckts / total_bytes, sequence.c:12-14,
+633-642): per-sequence {packets, bytes} of the timed steps, all-reduced once
+over RCCL at the end of the timed region.  Under torchrun the process group is
+created at every world size, 1 included, so the RCCL path runs on one GPU too.
 
 Prints ONE JSON line on rank 0.  The 1500-B variant, the D2H-inclusive rate
-into 4 KiB UMEM slots and the measured write-only peak ride along as extra
-keys.  The CPU oracle (oracle/, the checker) is timed beside it on the host
-cores as cpu_baseline — it is never the thing measured.
+into 4 KiB UMEM slots and the write-roofline probe ride along as extra keys.
+The CPU oracle (oracle/, the checker) is timed beside it on the host cores as
+cpu_baseline — it is never the thing measured.
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -34,6 +41,8 @@ from pbgpu import GpuContext, Sequence  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 HBM_ACHIEVABLE_GBPS = 6300.0  # the same guide's "≈6.3 TB/s achievable" (HBM section)
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r02.json")
+MIX = ("c2_udp_64", "c4_tcp_syn", "c5_icmp_echo")  # configs[4]'s three sequences (pb_configs.c5_mix)
 
 
 def parse():
@@ -43,23 +52,32 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--ramp-seconds", type=float, default=0.5,
                     help="untimed build launches before the warm-up steps, until the GPU clock has ramped")
-    ap.add_argument("--packets", type=int, default=1 << 25, help="packets per launch (per GPU)")
-    ap.add_argument("--config", default="c2_udp_64")
-    ap.add_argument("--no-variants", action="store_true", help="skip the 1500-B / D2H / fill extras")
+    ap.add_argument("--packets", type=int, default=None,
+                    help="iterations per launch per GPU (default 2^25; 2^24 per sequence for c5_mix)")
+    ap.add_argument("--config", default="c2_udp_64",
+                    choices=["c2_udp_64", "c2_udp_1500", "c3_udp_var", "c4_tcp_syn", "c5_icmp_echo", "c5_mix"])
+    ap.add_argument("--no-variants", action="store_true", help="skip the 1500-B / D2H extras")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
-                    help="committed rocprofv3 --pmc summary giving HBM bytes per launch")
-    return ap.parse_args()
+    ap.add_argument("--pmc", default=PMC_FILE, help="committed rocprofv3 --pmc summary giving HBM bytes per launch")
+    a = ap.parse_args()
+    if a.packets is None:
+        a.packets = (1 << 24) if a.config == "c5_mix" else (1 << 25)
+    return a
 
 
 def init_dist(n_gpus):
+    """torchrun (WORLD_SIZE in the environment): RCCL process group at any world
+    size; a plain `python bench.py` run is one rank without a process group."""
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n_gpus:
         raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    if n_gpus > 1 and not launched:
+        raise SystemExit("--gpus N > 1 runs under torch.distributed.run (one process per GPU)")
     dist = None
-    if world > 1:
+    if launched:
         import torch
         import torch.distributed as dist  # noqa: F811
 
@@ -76,58 +94,70 @@ def barrier(dist, local):
         torch.cuda.synchronize(local)
 
 
-def run_config(ctx, name, seq_idx, n_pkts, steps, warmup, rank, world, dist, local, ramp_s=0.0):
-    """Warm up, then time exactly `steps` launches; returns per-rank timings.
+def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ramp_s=0.0):
+    """Warm up, then time exactly `steps` steps; a step builds `n_pkts` iterations
+    of every sequence in `names` (one launch each).  Returns per-rank timings and
+    the all-reduced counters of the timed steps.
 
     The GPU starts a run below its sustained clock: the same 2-GiB launch took
     0.36-0.37 ms for the first ~10 ms of back-to-back launches and 0.30-0.31 ms
     after (scripts/alloc_probe.py), so untimed launches run for `ramp_s` seconds
     before the warm-up steps and the timed region sees the steady state a
     continuously sending generator runs in."""
-    seq = Sequence.from_config(pc.get(name))
-    ctx.load_sequence(seq_idx, seq, pc.SEED_BASE)
-    fb = ctx.alloc_frames(*ctx.build_size(seq_idx, n_pkts))
+    nseq = len(names)
+    bufs = []
+    for i, name in enumerate(names):
+        seq = Sequence.from_config(pc.get(name))
+        ctx.load_sequence(i, seq, pc.SEED_BASE)
+        bufs.append(ctx.alloc_frames(*ctx.build_size(i, n_pkts)))
     # span timing: one HIP-event pair around the timed launches, none per launch
     # (a per-launch pair writes back the L2 twice per launch: ~9 us gaps, DESIGN.md §7)
     ctx.set_timing(ctx.TIMING_SPAN)
     step_iter = lambda s: pb_dist.step_first_iter(s, rank, world, n_pkts)  # noqa: E731
+
+    def step(s):
+        for i in range(nseq):
+            ctx.build(i, step_iter(s), n_pkts, bufs[i])
+
     t_ramp = time.perf_counter()
     while time.perf_counter() - t_ramp < ramp_s:
         for s in range(8):
-            ctx.build(seq_idx, step_iter(s), n_pkts, fb)
+            step(s)
         ctx.sync()
     for s in range(warmup):
-        ctx.build(seq_idx, step_iter(s), n_pkts, fb)
+        step(s)
     ctx.sync()
     ctx.kernel_time()  # drop warm-up launches
-    p0, b0 = ctx.counters(seq_idx + 1)
+    p0, b0 = ctx.counters(nseq)
     barrier(dist, local)
     t0 = time.perf_counter()
     for s in range(steps):
-        ctx.build(seq_idx, step_iter(warmup + s), n_pkts, fb)
+        step(warmup + s)
     ctx.sync()
+    p1, b1 = ctx.counters(nseq)
+    dp = [int(x) for x in (p1 - p0)]
+    db = [int(x) for x in (b1 - b0)]
     counters = None
     if dist is not None:
-        p, b = ctx.counters(seq_idx + 1)
-        # RCCL over xGMI: the global sent-packet / byte counter
-        gp, gb = pb_dist.allreduce_counters([p[seq_idx]], [b[seq_idx]], device=f"cuda:{local}")
-        counters = [gp[0], gb[0]]
+        # RCCL over xGMI: the global sent-packet / byte counters of the timed steps
+        gp, gb = pb_dist.allreduce_counters(dp, db, device=f"cuda:{local}")
+        counters = {"packets": gp, "bytes": gb}
     barrier(dist, local)
     wall = time.perf_counter() - t0
     k_ms, k_n = ctx.kernel_time()
-    flen = int(fb.f.fixed_len)
-    p1, b1 = ctx.counters(seq_idx + 1)
-    bytes_per_launch = int(b1[seq_idx] - b0[seq_idx]) // steps  # this rank's frame bytes per launch
-    kernel = ctx.kernel_name(seq_idx)
-    fb.free()
+    flens = [int(fb.f.fixed_len) for fb in bufs]
+    kernels = [ctx.kernel_name(i) for i in range(nseq)]
+    for fb in bufs:
+        fb.free()
     if dist is not None:
         import torch
 
         w = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
-    return {"wall_s": wall, "kernel_ms_avg": k_ms / max(k_n, 1), "kernel_launches": k_n, "flen": flen,
-            "counters": counters, "bytes_per_launch": bytes_per_launch, "kernel": kernel}
+    return {"wall_s": wall, "span_ms_per_step": k_ms / max(steps, 1), "kernel_launches": k_n, "flens": flens,
+            "counters": counters, "packets_per_step": sum(dp) // steps, "bytes_per_step": sum(db) // steps,
+            "per_seq_bytes_per_step": [x // steps for x in db], "kernels": kernels}
 
 
 def d2h_rate(ctx, seq_idx, n_pkts):
@@ -152,14 +182,39 @@ def d2h_rate(ctx, seq_idx, n_pkts):
             "frame_gbps": frame_bytes / dt / 1e9}
 
 
+def host_cpu():
+    """The host the CPU baseline runs on: model, logical CPUs, the CPUs this process
+    may use and the cgroup CPU quota (the GPU box shares a large host)."""
+    model = platform.processor() or "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(name, budget_s, threads=None, faithful=True):
     """The CPU oracle on the host cores, frames copied into 4 KiB UMEM slots.
     faithful: a clock read and the rand_ip dotted-string round trip per
-    iteration, as sequence.c:434-497 does; lean: integer only."""
+    iteration, as sequence.c:434-497 does; lean: integer only.
+    Default threads: every CPU this process may run on (sched_getaffinity)."""
     import oracle_binding as ob
 
     if threads is None:
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        threads = max(1, len(os.sched_getaffinity(0)))
     seq = Sequence.from_config(pc.get(name))
     n = 20000 * threads
     ring = 4096  # NUM_FRAMES slots per socket, af_xdp.h:23
@@ -178,12 +233,16 @@ def cpu_baseline(name, budget_s, threads=None, faithful=True):
                       f"4096 x 4096-B UMEM slots), {threads} pthreads, {dt:.2f} s", "gbps": tot / dt / 1e9}
 
 
-def pmc_traffic(path, name):
+def pmc_traffic(path, names, packets):
+    """HBM bytes per step from a committed rocprofv3 --pmc summary (not measured in
+    this run), scaled from the PMC pass's packets per launch to `packets`."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("per_launch_hbm_bytes", {}).get(name)
-    except (OSError, ValueError):
+        hbm, pk = d.get("per_launch_hbm_bytes", {}), d.get("packets_per_launch", {})
+        vals = [hbm[n] * packets / pk.get(n, packets) for n in names]
+        return int(sum(vals))
+    except (OSError, ValueError, KeyError):
         return None
 
 
@@ -191,40 +250,45 @@ def main():
     a = parse()
     dist, world, rank, local = init_dist(a.gpus)
     ctx = GpuContext(local)
-    res = run_config(ctx, a.config, 0, a.packets, a.steps, a.warmup, rank, world, dist, local, a.ramp_seconds)
-    flen = res["flen"]
-    bpl = res["bytes_per_launch"]  # frame bytes one launch builds on one GPU
-    pkts_total = a.packets * a.steps * world
+    names = list(MIX) if a.config == "c5_mix" else [a.config]
+    res = run_configs(ctx, names, a.packets, a.steps, a.warmup, rank, world, dist, local, a.ramp_seconds)
+    bps = res["bytes_per_step"]  # frame bytes one step builds on one GPU
+    pkts_total = res["packets_per_step"] * a.steps * world
     wall = res["wall_s"]
     mpps = pkts_total / wall / 1e6
-    gbps = bpl * a.steps * world / wall / 1e9
-    k_s = res["kernel_ms_avg"] * 1e-3
-    achieved = bpl / k_s / 1e9
+    gbps = bps * a.steps * world / wall / 1e9
+    achieved = bps / (res["span_ms_per_step"] * 1e-3) / 1e9
     extra = {}
     peak_probe = None
     if rank == 0:
-        fill_ms = ctx.fill_probe(bpl, 20)
-        peak_probe = bpl / (fill_ms * 1e-3) / 1e9
+        shapes, best = ctx.fill_probe_shapes(bps, 20)
+        peak_probe = bps / (shapes[best] * 1e-3) / 1e9
         extra["write_peak_probe_gbps"] = round(peak_probe, 1)
-    if not a.no_variants:
+        extra["write_peak_probe_shape"] = best
+        extra["write_peak_probe_shapes_gbps"] = {k: round(bps / (v * 1e-3) / 1e9, 1) for k, v in shapes.items()}
+    if not a.no_variants and a.config == "c2_udp_64":
         steps15 = max(3, a.steps // 4)
-        v = run_config(ctx, "c2_udp_1500", 1, a.packets, steps15, 1, rank, world, dist, local, a.ramp_seconds / 2)
-        n1500 = a.packets * steps15 * world
-        ach15 = v["bytes_per_launch"] / (v["kernel_ms_avg"] * 1e-3) / 1e9
+        v = run_configs(ctx, ["c2_udp_1500"], a.packets, steps15, 1, rank, world, dist, local, a.ramp_seconds / 2)
+        n1500 = v["packets_per_step"] * steps15 * world
+        ach15 = v["bytes_per_step"] / (v["span_ms_per_step"] * 1e-3) / 1e9
         extra["udp_1500"] = {
             "mpps": round(n1500 / v["wall_s"] / 1e6, 3),
-            "gbps": round(v["bytes_per_launch"] * steps15 * world / v["wall_s"] / 1e9, 2),
-            "kernel": v["kernel"], "kernel_ms_avg": round(v["kernel_ms_avg"], 4),
+            "gbps": round(v["bytes_per_step"] * steps15 * world / v["wall_s"] / 1e9, 2),
+            "kernel": v["kernels"][0], "kernel_ms_avg": round(v["span_ms_per_step"], 4),
             "roofline_achieved_gbps": round(ach15, 1), "roofline_frac": round(ach15 / HBM_PEAK_GBPS, 4),
             "frac_of_guide_achievable": round(ach15 / HBM_ACHIEVABLE_GBPS, 4),
-            "traffic": pmc_traffic(a.pmc, "c2_udp_1500"), "algorithmic_bytes_per_launch": v["bytes_per_launch"],
-            "packets_per_launch": a.packets}
+            "frac_of_measured_write_peak": round(ach15 / peak_probe, 4) if peak_probe else None,
+            "traffic": pmc_traffic(a.pmc, ["c2_udp_1500"], a.packets), "traffic_source": os.path.relpath(a.pmc, ROOT),
+            "algorithmic_bytes_per_launch": v["bytes_per_step"], "packets_per_launch": a.packets}
         if rank == 0:
+            ctx.load_sequence(0, Sequence.from_config(pc.get("c2_udp_64")), pc.SEED_BASE)
+            ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
             extra["d2h_umem_64B"] = d2h_rate(ctx, 0, a.packets)
             extra["d2h_umem_1500B"] = d2h_rate(ctx, 1, a.packets)
     ctx.close()
     if rank != 0:
         return
+    doc = " ".join((pc.c5_mix if a.config == "c5_mix" else pc.BASELINE[a.config]).__doc__.split())
     line = {
         "metric": "device-resident Mpps & GB/s, 64B and 1500B UDP, L3+L4 checksums on",
         "value": round(mpps, 3),
@@ -239,29 +303,38 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seed stream splitmix64(0x5EEDBA5E ^ (seq<<48) + k); SURVEY.md §8d C2)",
-        "config": {"workload": f"{a.config}: " + " ".join((pc.BASELINE.get(a.config) or pc.c2_udp_64).__doc__.split()),
+        "data": "synthetic (seed stream splitmix64(0x5EEDBA5E ^ (seq<<48) + k); SURVEY.md §8d)",
+        "config": {"workload": f"{a.config}: {doc}",
+                   "sequences": names,
                    "packets_per_launch_per_gpu": a.packets,
-                   "frame_bytes": flen or None, "bytes_per_launch_per_gpu": bpl,
+                   "frame_bytes": res["flens"][0] if len(names) == 1 and res["flens"][0] else None,
+                   "bytes_per_step_per_gpu": bps,
                    "parallelism": f"shard-by-iteration x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac_of_guide_achievable": round(achieved / HBM_ACHIEVABLE_GBPS, 4),
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": pmc_traffic(a.pmc, a.config), "kernel": res["kernel"],
-                     "kernel_ms_avg": round(res["kernel_ms_avg"], 5),
-                     "algorithmic_bytes_per_launch": bpl,
-                     "frac_of_measured_write_peak": round(achieved / peak_probe, 4) if peak_probe else None},
+                     "frac_of_guide_achievable": round(achieved / HBM_ACHIEVABLE_GBPS, 4),
+                     "frac_of_measured_write_peak": round(achieved / peak_probe, 4) if peak_probe else None,
+                     "traffic": pmc_traffic(a.pmc, names, a.packets), "traffic_source": os.path.relpath(a.pmc, ROOT),
+                     "kernel": res["kernels"][0] if len(names) == 1 else res["kernels"],
+                     "kernel_ms_avg": round(res["span_ms_per_step"], 5),
+                     "algorithmic_bytes_per_launch": bps},
     }
     if res["counters"] is not None:
-        line["global_counters"] = {"packets": res["counters"][0], "bytes": res["counters"][1]}
+        line["global_counters"] = res["counters"]
+        line["global_counters"]["sequences"] = names
     line.update(extra)
     if world == 1 and a.cpu_seconds > 0:
-        line["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
-        # the other CPU-path points SURVEY.md §8d names: one thread, and the integer-only form
+        line["cpu_baseline"] = cpu_baseline(names[0], a.cpu_seconds)
+        line["cpu_baseline"]["host"] = host_cpu()
+        # the other CPU-path points SURVEY.md §8d names: one thread, the integer-only
+        # form, and configs[0] (static 64-B UDP, fixed source, one thread)
         short = max(1.0, a.cpu_seconds / 4)
         line["cpu_baseline_variants"] = {
-            "faithful_1_thread": cpu_baseline(a.config, short, threads=1),
-            "lean_all_threads": cpu_baseline(a.config, short, faithful=False)}
+            "faithful_1_thread": cpu_baseline(names[0], short, threads=1),
+            "lean_all_threads": cpu_baseline(names[0], short, faithful=False),
+            "configs0_c1_udp_static_64_1_thread": dict(
+                cpu_baseline("c1_udp_static_64", short, threads=1),
+                af_xdp_send="not measured: no AF_XDP socket / CAP_NET_RAW on the GPU host (BASELINE.md §3)")}
     print(json.dumps(line))
 
 

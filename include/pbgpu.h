@@ -60,7 +60,7 @@ typedef struct pbgpu_frames
 {
     uint8_t *data;          /* device pointer, capacity_bytes (16-B padded) */
     uint64_t *offsets;      /* device pointer, capacity_frames + 1 entries */
-    uint32_t *tile_first;   /* device scratch (variable-length tiling) */
+    void *reserved;         /* unused (keeps the layout of earlier builds) */
     uint64_t *scan_tmp;     /* device scratch (length scan) */
     uint64_t capacity_frames;
     uint64_t capacity_bytes;
@@ -136,12 +136,17 @@ int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq);
 #define PBGPU_TIMING_SPAN 1
 int pbgpu_set_timing(pbgpu_ctx *ctx, int mode);
 int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches);
-/* Write-only roofline probe: `reps` launches of each of three 16-B/lane fill
- * shapes over `bytes` (16 KiB per workgroup plain / non-temporal, 4 KiB per
- * workgroup plain); returns the fastest shape's mean device time per launch. */
+/* Write-only roofline probe: `reps` launches (best of two trials) of each of
+ * PBGPU_FILL_SHAPES fill shapes over `bytes` — 16-B stores per lane at 16 / 4 /
+ * 8 KiB per workgroup, plain and non-temporal, workgroups per CU capped by LDS,
+ * and the runtime's hipMemsetD32Async (tools/wbench.hip found the fastest plain
+ * fills).  pbgpu_fill_probe returns the fastest shape's mean
+ * device time per launch; _ex returns every shape's and the fastest's index,
+ * pbgpu_fill_shape_name names a shape. */
+#define PBGPU_FILL_SHAPES 9
 int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_launch);
-/* Build-kernel tile size chosen for a sequence (bytes per workgroup). */
-int pbgpu_tile_bytes(pbgpu_ctx *ctx, uint16_t seq_idx, uint32_t *tile_bytes);
+int pbgpu_fill_probe_ex(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_shape, int *best_shape);
+const char *pbgpu_fill_shape_name(int shape);
 
 /* Name of the frame-build kernel variant a loaded sequence launches
  * (as rocprofv3 reports it). */

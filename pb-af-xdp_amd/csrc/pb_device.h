@@ -13,9 +13,6 @@
 #include <stdint.h>
 
 #define PB_WG 256                          // threads per workgroup (4 waves)
-#define PB_CPL 4                           // 16-B chunks per lane per tile
-#define PB_TILE_MAX (PB_WG * PB_CPL * 16)  // 16 KiB of output per workgroup
-#define PB_NF_MAX 260                      // frames touching one tile, max
 #define PB_IMG_DW 16                       // header image: 64 B per frame
 #define PB_IMG_STRIDE 20                   // dwords per frame image row in LDS (16 used + pad: conflict-free b128 rows)
 #define PB_JNEG 80                         // jump table starts at j = -80
@@ -24,6 +21,7 @@
 #define PB_LCG48_N 4200                    // lcg48[m] = L^(48 m), m < 4200 (> 16-B chunks of a 64 KiB frame)
 #define PB_XPG 4096                        // XCD-owned page bytes (pb_xsmall_kernel, pb_xpage_kernel)
 #define PB_XREG (PB_XPG + 256)             // LDS bytes per page region (128 B slack either side)
+#define PBK_FILL_SHAPES 9                  // write-roofline probe shapes (pbk_launch_fill)
 #define PB_XNP_MAX 8                       // pb_xsmall_kernel: pages per workgroup, 4 (64-B frames) or 8 (128-B)
 
 // glibc LCG
@@ -92,9 +90,6 @@ struct pb_kargs
     uint32_t fixed_len;     // 0 -> variable
     pb_div flen;            // division by fixed_len
     const uint64_t *offsets;
-    const uint32_t *tile_first;
-    uint32_t tile_bytes;
-    uint32_t n_tiles;
     uint8_t *out;
     unsigned long long *counters; // [2] pckts, bytes of this sequence
     uint32_t small_ndw;     // >0: small fixed frames, one lane per frame, NDW dwords per lane
@@ -131,6 +126,8 @@ struct pb_kargs
     uint32_t fst_dbg;       // diagnostics (PBGPU_FST_DBG, wrong output): bit 0 skips payload + headers,
                             // bit 1 the stores, bit 3 phase A (time decomposition);
                             // pb_vstage_kernel: bit 4 fixed 8-lane groups, bit 5 no 32-lane groups (A/B)
+    uint32_t lds_pad;       // dynamic LDS added to the build launch: caps workgroups per CU (fewer
+                            // concurrent writers)
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

@@ -21,13 +21,13 @@
 #include "../../include/pbgpu.h"
 #include "pb_device.h"
 
-extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid, hipStream_t st);
+extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st);
 extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
-                                         uint64_t *offsets, uint32_t *tile_first, uint32_t tile_shift,
-                                         hipStream_t st);
+                                         uint64_t *offsets, hipStream_t st);
 extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *offsets, uint64_t first, uint32_t n,
                                          uint8_t *dst, uint32_t stride, uint16_t *lens, hipStream_t st);
 extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipStream_t st);
+extern "C" const char *pbk_fill_shape_name(int mode);
 extern "C" hipError_t pbk_launch_scatter_fixed(const uint8_t *src, uint32_t flen, uint32_t n, uint8_t *dst,
                                                uint32_t stride, hipStream_t st);
 
@@ -76,7 +76,6 @@ struct seq_slot
     pb_kargs K;              // template part; per-launch fields patched in pbgpu_build
     uint32_t fpi = 1;        // frames per iteration
     uint32_t min_flen = 0, max_flen = 0;
-    uint32_t tile_shift = 14;
     uint2 *d_ranges = nullptr;
     pb_pl *d_pls = nullptr;
     uint8_t *d_blob = nullptr;
@@ -705,11 +704,8 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         }
     }
     {
-        const char *kern = getenv("PBGPU_KERNEL"); // "tile": force the tile kernel (comparison only)
-        const bool tile = kern && !strcmp(kern, "tile");
-        if (tile)
-            K.small_ndw = 0;
-        else if (!K.small_ndw)
+        const char *kern = getenv("PBGPU_KERNEL");
+        if (!K.small_ndw)
         {
             // lanes per frame (measured, profiles/r01/gsweep): equal-length frames take
             // the group size that wastes the fewest lanes on the frame's chunk count,
@@ -873,14 +869,6 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             }
         }
     }
-    // tile: power of two, <= 16 KiB, <= (PB_NF_MAX - 2) frames of minimum length
-    uint32_t cap = (PB_NF_MAX - 2) * minf;
-    uint32_t shift = 14;
-    while (shift > 4 && (1u << shift) > cap)
-        --shift;
-    S.tile_shift = shift;
-    K.tile_bytes = 1u << shift;
-
     int rc;
     if ((rc = upload(&S.d_ranges, ranges.data(), ranges.size())) != PBGPU_OK)
         return rc;
@@ -895,6 +883,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     K.jump = ctx->d_jump;
     K.lcg48 = ctx->d_lcg48;
     K.counters = ctx->d_counters + 4 * seq_idx;
+    K.lds_pad = (uint32_t)env_int("PBGPU_LDS_PAD", (int)K.lds_pad);
     S.K = K;
     S.loaded = true;
     return PBGPU_OK;
@@ -924,12 +913,10 @@ int pbgpu_frames_alloc(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capaci
     if (f == NULL)
         return PBGPU_ENOMEM;
     capacity_bytes = (capacity_bytes + 15) & ~15ull;
-    const uint64_t max_tiles = capacity_bytes / 4096 + 4; // tiles are >= 8 KiB (frames >= 42 B)
     const uint64_t nblocks = capacity_frames / PB_SCAN_FRAMES_PER_BLOCK + 1;
     // +64 B: word-granular readers (UMEM scatter) may touch a few bytes past the last frame
     if (hipMalloc((void **)&f->data, capacity_bytes + 64) != hipSuccess ||
         hipMalloc((void **)&f->offsets, (capacity_frames + 1) * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc((void **)&f->tile_first, max_tiles * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&f->scan_tmp, nblocks * sizeof(uint64_t)) != hipSuccess)
     {
         pbgpu_frames_free(ctx, f);
@@ -955,8 +942,6 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
         (void)hipFree(f->data);
     if (f->offsets)
         (void)hipFree(f->offsets);
-    if (f->tile_first)
-        (void)hipFree(f->tile_first);
     if (f->scan_tmp)
         (void)hipFree(f->scan_tmp);
     free(f);
@@ -1030,7 +1015,6 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     K.n_frames = nf;
     K.out = out->data;
     K.offsets = out->offsets;
-    K.tile_first = out->tile_first;
     out->seq_idx = seq_idx;
     out->first_iter = first_iter;
     out->n_frames = nf;
@@ -1040,24 +1024,18 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         out->total_bytes = 0;
         return PBGPU_OK;
     }
-    uint64_t n_tiles;
     if (K.fixed_len)
     {
         K.total_bytes = nf * K.fixed_len;
         out->total_bytes = K.total_bytes;
-        n_tiles = (K.total_bytes + K.tile_bytes - 1) >> S.tile_shift;
     }
     else
     {
         out->total_bytes = UINT64_MAX;
-        n_tiles = (max_bytes + K.tile_bytes - 1) >> S.tile_shift;
         const uint64_t nblocks = (nf + PB_SCAN_FRAMES_PER_BLOCK - 1) / PB_SCAN_FRAMES_PER_BLOCK;
         HIPCHK(pbk_launch_lengths(&K, (unsigned long long *)out->scan_tmp, (uint32_t)nblocks, out->offsets,
-                                  out->tile_first, S.tile_shift, ctx->stream));
+                                  ctx->stream));
     }
-    if (n_tiles > 0x7FFFFFFFull)
-        return PBGPU_ENOSPC;
-    K.n_tiles = (uint32_t)n_tiles;
     K.xs_grid = 0;
     if (K.small_ndw && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && !env_is("PBGPU_KERNEL", "linear"))
     {
@@ -1102,12 +1080,12 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             }
             HIPCHK(hipEventRecord(ctx->span.a, ctx->stream));
         }
-        HIPCHK(pbk_launch_build(&K, (uint32_t)n_tiles, ctx->stream));
+        HIPCHK(pbk_launch_build(&K, ctx->stream));
         ++ctx->span_n;
         return PBGPU_OK;
     }
     HIPCHK(hipEventRecord(tp.a, ctx->stream));
-    HIPCHK(pbk_launch_build(&K, (uint32_t)n_tiles, ctx->stream));
+    HIPCHK(pbk_launch_build(&K, ctx->stream));
     HIPCHK(hipEventRecord(tp.b, ctx->stream));
     if (timing)
         report_phase_timing(ctx, n_wg);
@@ -1232,6 +1210,14 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
     }
     // variable length: a scatter kernel writes straight into registered
     // (mapped) UMEM; unregistered memory goes through a pinned staging copy.
+    // A frame longer than a slot would overrun the next slot (or, in the last
+    // slot, the UMEM allocation): refused up front from the sequence's longest
+    // frame, as the fixed-length path refuses fixed_len > slot_stride (the
+    // reference does not check, af_xdp.c:214).
+    if (f->seq_idx >= PB_MAX_SEQUENCES || !ctx->seqs[f->seq_idx].loaded)
+        return PBGPU_EINVAL;
+    if (ctx->seqs[f->seq_idx].max_flen > slot_stride)
+        return PBGPU_EINVAL;
     void *dev_dst = NULL;
     uint16_t *d_lens = NULL;
     if (hipHostGetDevicePointer(&dev_dst, dst, 0) == hipSuccess && dev_dst != NULL)
@@ -1357,7 +1343,7 @@ int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches)
     return PBGPU_OK;
 }
 
-int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_launch)
+int pbgpu_fill_probe_ex(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_shape, int *best_shape)
 {
     if (ctx == NULL || bytes < 16 || reps == 0)
         return PBGPU_EINVAL;
@@ -1368,34 +1354,48 @@ int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_p
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     double best = 1e30;
-    for (int mode = 0; mode < 3; ++mode) // the store shapes of pbk_launch_fill; report the fastest
+    int bi = 0;
+    for (int mode = 0; mode < PBGPU_FILL_SHAPES; ++mode) // pbk_launch_fill's shapes; the fastest is the peak
     {
-        HIPCHK(pbk_launch_fill(buf, bytes, mode, ctx->stream)); // warm-up
-        HIPCHK(hipEventRecord(a, ctx->stream));
-        for (uint32_t r = 0; r < reps; ++r)
-            HIPCHK(pbk_launch_fill(buf, bytes, mode, ctx->stream));
-        HIPCHK(hipEventRecord(b, ctx->stream));
-        HIPCHK(hipEventSynchronize(b));
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, a, b));
-        best = ms / reps < best ? ms / reps : best;
+        double mode_best = 1e30;
+        for (int trial = 0; trial < 2; ++trial)
+        {
+            HIPCHK(pbk_launch_fill(buf, bytes, mode, ctx->stream)); // warm-up
+            HIPCHK(hipEventRecord(a, ctx->stream));
+            for (uint32_t r = 0; r < reps; ++r)
+                HIPCHK(pbk_launch_fill(buf, bytes, mode, ctx->stream));
+            HIPCHK(hipEventRecord(b, ctx->stream));
+            HIPCHK(hipEventSynchronize(b));
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, a, b));
+            mode_best = ms / reps < mode_best ? ms / reps : mode_best;
+        }
+        if (ms_per_shape)
+            ms_per_shape[mode] = mode_best;
+        if (mode_best < best)
+            best = mode_best, bi = mode;
     }
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     (void)hipFree(buf);
-    if (ms_per_launch)
-        *ms_per_launch = best;
+    if (best_shape)
+        *best_shape = bi;
     return PBGPU_OK;
 }
 
-int pbgpu_tile_bytes(pbgpu_ctx *ctx, uint16_t seq_idx, uint32_t *tile_bytes)
+int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_launch)
 {
-    if (ctx == NULL || seq_idx >= PB_MAX_SEQUENCES || tile_bytes == NULL)
-        return PBGPU_EINVAL;
-    if (!ctx->seqs[seq_idx].loaded)
-        return PBGPU_ENOENT;
-    *tile_bytes = ctx->seqs[seq_idx].K.tile_bytes;
-    return PBGPU_OK;
+    double ms[PBGPU_FILL_SHAPES];
+    int bi = 0;
+    const int rc = pbgpu_fill_probe_ex(ctx, bytes, reps, ms, &bi);
+    if (rc == PBGPU_OK && ms_per_launch)
+        *ms_per_launch = ms[bi];
+    return rc;
+}
+
+const char *pbgpu_fill_shape_name(int shape)
+{
+    return pbk_fill_shape_name(shape);
 }
 
 int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
@@ -1414,13 +1414,11 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
-    else if (K.small_ndw)
+    else
         snprintf(buf, n, "%s<%u, %u, %s>",
                  K.xs_np && !env_is("PBGPU_KERNEL", "linear") ? (K.xp ? "pb_xpage_kernel" : "pb_xsmall_kernel")
                                                                : "pb_small_kernel",
                  K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
-    else
-        snprintf(buf, n, "pb_build_kernel<%s>", K.fixed_len ? "true" : "false");
     return PBGPU_OK;
 }
 

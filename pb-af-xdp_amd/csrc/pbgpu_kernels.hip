@@ -1,29 +1,20 @@
 // pbgpu_kernels.hip — MI355X (gfx950) frame-build kernels.
 //
 // Hot path: PB-AF-XDP thread_hdl() loop body, src/sequence.c:433-602, for a
-// batch of iterations at once.  One workgroup owns one TILE of the packed
-// output stream (a power-of-two byte range, <= 16 KiB) and writes every
-// 16-B chunk of it exactly once with an aligned non-temporal dwordx4 store,
-// whatever the frame lengths and alignments are:
-//
-//   phase A  one lane per frame touching the tile: seed -> r0 -> TTL / ID /
-//            source IP / ports / payload length (sequence.c:434-527, 548),
-//            header image (sequence.c:150-258) with IPv4 checksum
-//            (sequence.c:596-602) into LDS, L4 header + pseudo-header sum.
-//   phase B  one lane per 16-B chunk: payload bytes (glibc rand_r low byte,
-//            sequence.c:552-555) generated directly in output alignment with
-//            a jump table + 24-bit LCG steps; per-frame payload word sums
-//            accumulated in LDS (csum_partial, sequence.c:572/581/590).
-//            Payload that spills past the tile is summed (not stored) so the
-//            tile that holds a frame's checksum field can finish it.
-//   phase C  one lane per frame: fold + complement the L4 checksum into the
-//            header image (csum_tcpudp_magic / icmp_csum).
-//   phase D  one lane per chunk: OR the header bytes of the (at most two)
-//            frames overlapping the chunk into its payload bytes, store.
-//
+// batch of iterations at once: per frame the seed -> r0 -> TTL / ID / source IP
+// / ports / payload length (sequence.c:434-527, 548), the header image
+// (sequence.c:150-258), the payload bytes (glibc rand_r low byte,
+// sequence.c:552-555, in 24-bit LCG arithmetic), the L4 checksum
+// (csum_tcpudp_magic / icmp_csum, sequence.c:563-594) and tot_len + the IPv4
+// checksum (sequence.c:596-602), written packed into HBM.  Kernel by frame
+// shape (selection in pbgpu_load_sequence):
+//   pb_xsmall_kernel / pb_xpage_kernel / pb_small_kernel   frames <= 128 B, one lane per frame
+//   pb_fstage_kernel                                      fixed length > 128 B, random payload
+//   pb_vstage_kernel                                      packed variable length, random payload
+//   pb_stage_kernel                                       static / mixed payloads, the literal rule
+//   pb_gpf_kernel                                         frames too long for an LDS stage
 // The template, CIDR table pointers and divisors arrive as kernel arguments
-// (scalar registers); header images, per-frame records and the chunk->frame
-// map live in LDS.  No inter-workgroup communication; no atomics to HBM
+// (scalar registers); no inter-workgroup communication; no atomics to HBM
 // except two counter adds per launch.
 #include "pb_device.h"
 
@@ -258,277 +249,6 @@ __device__ __forceinline__ uint32_t pb_header(const pb_kargs &K, uint32_t r0, ui
 // One payload byte = three glibc LCG steps: x -> A3 * x + C3 (mod 2^32).
 constexpr uint32_t PB_A3 = PB_LCG_A * PB_LCG_A * PB_LCG_A;
 constexpr uint32_t PB_C3 = PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u);
-
-template <bool FIXED>
-__global__ __launch_bounds__(PB_WG) void pb_build_kernel(pb_kargs K)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t s_img[PB_NF_MAX * PB_IMG_STRIDE];
-    __shared__ int32_t s_rel[PB_NF_MAX];     // frame offset relative to tile start
-    __shared__ uint32_t s_nv[PB_NF_MAX];     // nvalid | random << 31
-    __shared__ uint32_t s_src[PB_NF_MAX];    // st0 (random) or blob_off (static)
-    __shared__ uint32_t s_hsum[PB_NF_MAX];   // L4 header + pseudo header + frame-aligned payload sum
-    __shared__ uint32_t s_psc[PB_NF_MAX];    // payload sum from chunks (output alignment)
-    __shared__ uint16_t s_map[FIXED ? 1 : PB_TILE_MAX / 16]; // chunk -> frame holding its first byte
-    __shared__ uint32_t s_nvirt, s_vframe;
-
-    const uint32_t tid = threadIdx.x;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t flags = K.flags;
-    const uint64_t tile_start = (uint64_t)tile * K.tile_bytes;
-    const uint64_t total = FIXED ? K.total_bytes : K.offsets[K.n_frames];
-    if (tile_start >= total)
-        return; // variable length: grid sized for the upper bound
-    const uint32_t tile_len = (uint32_t)min((uint64_t)K.tile_bytes, total - tile_start);
-    const uint32_t nchunks = (tile_len + 15u) >> 4;
-
-    uint64_t fa, fb;
-    if (FIXED)
-    {
-        fa = tile_start / K.fixed_len;
-        fb = (tile_start + tile_len - 1) / K.fixed_len;
-    }
-    else
-    {
-        fa = K.tile_first[tile];
-        fb = K.tile_first[tile + 1];
-    }
-    uint32_t nf = (uint32_t)(fb - fa + 1);
-    if (nf > PB_NF_MAX)
-    {
-        if (tid == 0)
-            atomicAdd(K.counters + 2, 1ull); // host sizing bug: flagged, never silent
-        nf = PB_NF_MAX;
-    }
-
-    if (tid == 0)
-    {
-        s_nvirt = 0;
-        s_vframe = 0;
-    }
-
-    // ---------------- phase A: one lane per frame ----------------
-    for (uint32_t lf = tid; lf < nf; lf += PB_WG)
-    {
-        const uint64_t f = fa + lf;
-        uint64_t off;
-        uint32_t flen;
-        if (FIXED)
-        {
-            off = f * K.fixed_len;
-            flen = K.fixed_len;
-        }
-        else
-        {
-            off = K.offsets[f];
-            flen = (uint32_t)(K.offsets[f + 1] - off);
-        }
-        const int32_t rel = (int32_t)((int64_t)off - (int64_t)tile_start);
-
-        uint64_t k;
-        uint32_t pi;
-        pb_frame_index(K, f, k, pi);
-        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
-        const uint32_t r0 = pb_rand_r(s);
-        const pb_frame_pl P = pb_payload(K, s, pi);
-
-        uint32_t d[16];
-        const uint32_t l4tot = pb_header(K, r0, P.plen, d, pb_range(K, r0));
-
-        // L4 header words (check field still 0) + pseudo header
-        uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) +
-                      pb_halves(d[12]) + pb_halves(d[13]);
-        if (flags & PBK_PSEUDO)
-            hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
-        if (!P.random)
-        {
-            hs += P.ssum;
-        }
-        else if (flags & PBK_SUM_IN_A)
-        {
-            uint32_t x = P.st0;
-            uint32_t ps = 0;
-            for (uint32_t j = 0; j < P.nvalid; ++j)
-            {
-                x = x * PB_LCG_A + PB_LCG_C;
-                x = x * PB_LCG_A + PB_LCG_C;
-                x = x * PB_LCG_A + PB_LCG_C;
-                ps += ((x >> 16) & 0xFFu) << ((j & 1u) << 3);
-            }
-            hs += ps;
-        }
-
-        uint4 *row = reinterpret_cast<uint4 *>(s_img + lf * PB_IMG_STRIDE);
-        row[0] = make_uint4(d[0], d[1], d[2], d[3]);
-        row[1] = make_uint4(d[4], d[5], d[6], d[7]);
-        row[2] = make_uint4(d[8], d[9], d[10], d[11]);
-        row[3] = make_uint4(d[12], d[13], d[14], d[15]);
-        row[4] = make_uint4(0u, 0u, 0u, 0u);
-        s_rel[lf] = rel;
-        s_nv[lf] = P.nvalid | (P.random << 31);
-        s_src[lf] = P.random ? P.st0 : P.blob_off;
-        s_hsum[lf] = hs;
-        s_psc[lf] = 0;
-
-        if (!FIXED)
-        {
-            int32_t c0 = rel <= 0 ? 0 : (rel + 15) >> 4;
-            int32_t c1 = (rel + (int32_t)flen - 1) >> 4;
-            if (c1 >= (int32_t)nchunks)
-                c1 = (int32_t)nchunks - 1;
-            for (int32_t c = c0; c <= c1; ++c)
-                s_map[c] = (uint16_t)lf;
-        }
-
-        // payload past the tile end of a frame whose checksum field is in this tile
-        if ((flags & PBK_L4_CSUM) && P.random && !(flags & PBK_SUM_IN_A))
-        {
-            const int32_t cpos = rel + (int32_t)(K.csum_dw * 4 + K.csum_hi * 2);
-            const int32_t span = (int32_t)(nchunks * 16);
-            if (cpos >= 0 && cpos < (int32_t)tile_len && rel + (int32_t)flen > span)
-            {
-                s_nvirt = (uint32_t)((rel + (int32_t)flen - span + 15) >> 4);
-                s_vframe = lf;
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---------------- phase B: payload bytes per 16-B chunk ----------------
-    const uint32_t a3 = PB_A3, c3 = PB_C3;
-    const bool chunk_sums = (flags & PBK_L4_CSUM) && !(flags & PBK_SUM_IN_A);
-    const int32_t hl = (int32_t)K.hl;
-
-    auto gen = [&](uint32_t a, int32_t pos, uint32_t (&o)[4]) {
-        o[0] = o[1] = o[2] = o[3] = 0u;
-        const int32_t rel = s_rel[a];
-        const uint32_t nv = s_nv[a];
-        const int32_t nvalid = (int32_t)(nv & 0x7FFFFFFFu);
-        const int32_t j0 = pos - rel - hl; // payload index of the chunk's first byte
-        if (j0 >= nvalid || j0 + 16 <= 0)
-            return;
-        const int lo = j0 < 0 ? -j0 : 0;
-        const int hi = (nvalid - j0) < 16 ? (nvalid - j0) : 16;
-        if (nv >> 31)
-        {
-            const uint2 jt = K.jump[j0 + PB_JNEG];
-            uint32_t x0 = jt.x * s_src[a] + jt.y;
-            uint32_t x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
-            o[0] = pb_pack4(x0, x1, x2, x3);
-            x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
-            o[1] = pb_pack4(x0, x1, x2, x3);
-            x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
-            o[2] = pb_pack4(x0, x1, x2, x3);
-            x0 = pb_step3(x3, a3, c3), x1 = pb_step3(x0, a3, c3), x2 = pb_step3(x1, a3, c3), x3 = pb_step3(x2, a3, c3);
-            o[3] = pb_pack4(x0, x1, x2, x3);
-        }
-        else
-        {
-            const uint8_t *b = K.blob + s_src[a] + j0;
-            const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)b & ~(uintptr_t)3);
-            const uint32_t sh = (uint32_t)((uintptr_t)b & 3);
-            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-            o[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            o[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-            o[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
-            o[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
-        }
-        if (lo > 0 || hi < 16)
-        {
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                o[t] &= pb_bytemask(lo, hi, t);
-        }
-        if (chunk_sums && (nv >> 31))
-        {
-            const uint32_t sum = pb_halves(o[0]) + pb_halves(o[1]) + pb_halves(o[2]) + pb_halves(o[3]);
-            atomicAdd(&s_psc[a], sum);
-        }
-    };
-
-    uint32_t data[PB_CPL][4];
-    uint32_t fr[PB_CPL];
-    const int32_t rel0 = s_rel[0];
-#pragma unroll
-    for (int ci = 0; ci < PB_CPL; ++ci)
-    {
-        const uint32_t c = tid + ci * PB_WG;
-        data[ci][0] = data[ci][1] = data[ci][2] = data[ci][3] = 0u;
-        fr[ci] = 0;
-        if (c < nchunks)
-        {
-            const uint32_t a = FIXED ? pb_divq((uint32_t)((int32_t)(c * 16) - rel0), K.flen) : (uint32_t)s_map[c];
-            fr[ci] = a;
-            gen(a, (int32_t)(c * 16), data[ci]);
-        }
-    }
-    {
-        const uint32_t nvirt = s_nvirt;
-        const uint32_t vf = s_vframe;
-        for (uint32_t v = tid; v < nvirt; v += PB_WG)
-        {
-            uint32_t tmp[4];
-            gen(vf, (int32_t)((nchunks + v) * 16), tmp);
-        }
-    }
-    __syncthreads();
-
-    // ---------------- phase C: finish L4 checksums ----------------
-    if (flags & PBK_L4_CSUM)
-    {
-        for (uint32_t lf = tid; lf < nf; lf += PB_WG)
-        {
-            uint32_t pc = pb_fold(s_psc[lf]);
-            if (s_rel[lf] & 1) // chunk sums were taken in output alignment
-                pc = pb_bswap16(pc);
-            const uint32_t c = (~pb_fold(pb_fold(s_hsum[lf]) + pc)) & 0xFFFFu;
-            s_img[lf * PB_IMG_STRIDE + K.csum_dw] |= K.csum_hi ? (c << 16) : c;
-        }
-    }
-    __syncthreads();
-
-    // ---------------- phase D: merge header bytes, store ----------------
-    uint8_t *const out = K.out + tile_start;
-#pragma unroll
-    for (int ci = 0; ci < PB_CPL; ++ci)
-    {
-        const uint32_t c = tid + ci * PB_WG;
-        if (c < nchunks)
-        {
-            const uint32_t a = fr[ci];
-            const int32_t pos = (int32_t)(c * 16);
-            const int32_t qc = pos - s_rel[a];
-            uint32_t o0 = data[ci][0], o1 = data[ci][1], o2 = data[ci][2], o3 = data[ci][3];
-            if (qc < hl)
-            {
-                const uint32_t *img = s_img + a * PB_IMG_STRIDE;
-                o0 |= pb_window(img, qc);
-                o1 |= pb_window(img, qc + 4);
-                o2 |= pb_window(img, qc + 8);
-                o3 |= pb_window(img, qc + 12);
-            }
-            if (a + 1 < nf)
-            {
-                const int32_t relb = s_rel[a + 1];
-                if (relb < pos + 16)
-                {
-                    const uint32_t *img = s_img + (a + 1) * PB_IMG_STRIDE;
-                    const int32_t xb = pos - relb;
-                    o0 |= pb_window(img, xb);
-                    o1 |= pb_window(img, xb + 4);
-                    o2 |= pb_window(img, xb + 8);
-                    o3 |= pb_window(img, xb + 12);
-                }
-            }
-            __builtin_nontemporal_store(pb_u32x4{o0, o1, o2, o3}, reinterpret_cast<pb_u32x4 *>(out + pos));
-        }
-    }
-
-    if (FIXED && tile == 0 && tid == 0)
-    {
-        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
-        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
-    }
-}
 
 // ---------------- small fixed-length frames: one lane per frame ----------------
 //
@@ -2073,7 +1793,7 @@ __global__ __launch_bounds__(1024) void pb_scan_blocks(unsigned long long *block
 }
 
 __global__ __launch_bounds__(256) void pb_len_scan(pb_kargs K, const unsigned long long *block_sums,
-                                                   uint64_t *offsets, uint32_t *tile_first, uint32_t tile_shift)
+                                                   uint64_t *offsets)
 {
     __shared__ unsigned long long s_v[256];
     const uint64_t base = (uint64_t)blockIdx.x * 256 * PB_SCAN_ITEMS + (uint64_t)threadIdx.x * PB_SCAN_ITEMS;
@@ -2103,14 +1823,6 @@ __global__ __launch_bounds__(256) void pb_len_scan(pb_kargs K, const unsigned lo
         if (f < K.n_frames)
         {
             offsets[f] = off;
-            // tiles whose first byte lies in this frame
-            const uint64_t tmask = (1ull << tile_shift) - 1;
-            const uint64_t t0 = (off + tmask) >> tile_shift;
-            const uint64_t t1 = (off + len[it] - 1) >> tile_shift;
-            for (uint64_t t = t0; t <= t1; ++t)
-                tile_first[t] = (uint32_t)f;
-            if (f == K.n_frames - 1)
-                tile_first[t1 + 1] = (uint32_t)f; // sentinel: fb of the last tile
             off += len[it];
         }
     }
@@ -2131,8 +1843,13 @@ __global__ __launch_bounds__(64) void pb_scatter_slots(const uint8_t *src, const
     uint32_t *d = reinterpret_cast<uint32_t *>(dst + (uint64_t)blockIdx.x * stride);
     const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)s & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
-    for (uint32_t i = threadIdx.x; i * 4 < len; i += 64)
+    // whole dwords, then the frame's last 1-3 bytes one by one: nothing is
+    // written past the frame's own bytes in its slot
+    for (uint32_t i = threadIdx.x; i * 4 + 4 <= len; i += 64)
         d[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+    const uint32_t tail = len & 3u, i = len >> 2;
+    if (threadIdx.x < tail)
+        reinterpret_cast<uint8_t *>(d + i)[threadIdx.x] = s[4 * i + threadIdx.x];
 }
 
 // fixed-length frames -> slots: thread (f, i) stores dword i of frame f (f = gid / dpf)
@@ -2186,7 +1903,7 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
 {
     if (K->xs_grid && K->xp)
     {
-        const size_t lds = (size_t)K->xs_np * PB_XREG;
+        const size_t lds = (size_t)K->xs_np * PB_XREG + K->lds_pad;
         const bool w512 = K->xp_wgt == 512;
         if (K->pl0.random && w512)
             hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, 512>), dim3(K->xs_grid), dim3(512), lds, st, *K);
@@ -2200,16 +1917,16 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
     else if (K->pl0.random)
     {
         if (K->xs_grid)
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), 0, st, *K);
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
         else
-            hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true>), dim3(grid), dim3(PB_WG), 0, st, *K);
+            hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true>), dim3(grid), dim3(PB_WG), K->lds_pad, st, *K);
     }
     else
     {
         if (K->xs_grid)
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false>), dim3(K->xs_grid), dim3(PB_WG), 0, st, *K);
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
         else
-            hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false>), dim3(grid), dim3(PB_WG), 0, st, *K);
+            hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false>), dim3(grid), dim3(PB_WG), K->lds_pad, st, *K);
     }
 }
 
@@ -2224,12 +1941,12 @@ static void pbk_launch_small(const pb_kargs *K, uint32_t grid, hipStream_t st)
         pbk_launch_small_p<NDW, 1>(K, grid, st);
 }
 
-extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid, hipStream_t st)
+extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
 {
     if (K->fst_g)
     {
         const uint32_t grid = (uint32_t)((K->n_frames + K->fst_wgf - 1) / K->fst_wgf);
-        const size_t lds = (size_t)K->fst_nbuf * K->fst_sb + PB_FST_LDS(K->fst_wgf);
+        const size_t lds = (size_t)K->fst_nbuf * K->fst_sb + PB_FST_LDS(K->fst_wgf) + K->lds_pad;
         const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
 #define PB_FST(GG)                                                                                    \
     do                                                                                                \
@@ -2281,7 +1998,7 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid,
     else if (K->stage_win && K->vst)
     {
         const uint32_t grid = (uint32_t)((K->n_frames + K->stage_wgf - 1) / K->stage_wgf);
-        const size_t lds = K->stage_bytes + PB_VST_LDS(K->stage_wgf);
+        const size_t lds = K->stage_bytes + PB_VST_LDS(K->stage_wgf) + K->lds_pad;
         const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
 #define PB_VST(GG)                                                                                    \
     do                                                                                                \
@@ -2304,7 +2021,7 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid,
     else if (K->stage_win)
     {
         const uint32_t grid = (uint32_t)((K->n_frames + K->stage_wgf - 1) / K->stage_wgf);
-        const size_t lds = K->stage_bytes + PB_STAGE_LDS(K->stage_wgf);
+        const size_t lds = K->stage_bytes + PB_STAGE_LDS(K->stage_wgf) + K->lds_pad;
         const uint32_t rm = K->gpf_rmode;
 #define PB_STG(GG, RM)                                                                                     \
     do                                                                                                     \
@@ -2348,22 +2065,19 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, uint32_t n_tiles_grid,
         else
             pbk_launch_small<32>(K, grid, st);
     }
-    else if (K->fixed_len)
-        hipLaunchKernelGGL(pb_build_kernel<true>, dim3(n_tiles_grid), dim3(PB_WG), 0, st, *K);
     else
-        hipLaunchKernelGGL(pb_build_kernel<false>, dim3(n_tiles_grid), dim3(PB_WG), 0, st, *K);
+        return hipErrorInvalidValue; // pbgpu_load_sequence selects one of the kernels above for every sequence
     return hipGetLastError();
 }
 
 extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
-                                         uint64_t *offsets, uint32_t *tile_first, uint32_t tile_shift,
-                                         hipStream_t st)
+                                         uint64_t *offsets, hipStream_t st)
 {
     hipLaunchKernelGGL(pb_len_reduce, dim3(nblocks), dim3(256), 0, st, *K, block_sums);
     hipLaunchKernelGGL(pb_scan_blocks, dim3(1), dim3(1024), 0, st, block_sums, nblocks, offsets, K->n_frames,
                        K->counters);
     hipLaunchKernelGGL(pb_len_scan, dim3(nblocks), dim3(256), 0, st, *K, (const unsigned long long *)block_sums,
-                       offsets, tile_first, tile_shift);
+                       offsets);
     return hipGetLastError();
 }
 
@@ -2384,18 +2098,58 @@ extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *off
     return hipGetLastError();
 }
 
-// write-roofline probe shapes: 0 = 16 KiB per workgroup (4 plain 16-B stores per lane),
-// 1 = the same with non-temporal stores, 2 = 4 KiB per workgroup (one plain store per lane)
+// 8 KiB per 512-thread workgroup, one plain 16-B store per lane
+__global__ __launch_bounds__(512) void pb_fill512_kernel(pb_u32x4 *dst, uint64_t n16, uint32_t v)
+{
+    const uint64_t c = (uint64_t)blockIdx.x * 512 + threadIdx.x;
+    if (c < n16)
+        dst[c] = pb_u32x4{v, v ^ (uint32_t)c, v, (uint32_t)c};
+}
+
+// Write-roofline probe shapes (tools/wbench.hip, profiles/r02/wbench: the fastest plain
+// fills found; dynamic LDS caps the workgroups per CU, and fewer concurrent writers
+// write faster down to 4 per CU):
+//  0  16 KiB per workgroup, 4 plain 16-B stores per lane     4  4 KiB, LDS-capped at 5 workgroups / CU
+//  1  the same, non-temporal                                 5  4 KiB, 4 workgroups / CU
+//  2  4 KiB per workgroup, one plain store per lane (8 / CU)  6  4 KiB, 3 workgroups / CU
+//  3  4 KiB, LDS-capped at 6 workgroups / CU                 7  8 KiB per 512-thread workgroup, 1 store / lane
+//  8  hipMemsetD32Async (the runtime's fill)
+extern "C" const char *pbk_fill_shape_name(int mode)
+{
+    static const char *names[PBK_FILL_SHAPES] = {
+        "16KiB/wg 4 st/lane", "16KiB/wg 4 st/lane nt", "4KiB/wg 1 st/lane (8 wg/CU)", "4KiB/wg 1 st/lane, 6 wg/CU",
+        "4KiB/wg 1 st/lane, 5 wg/CU", "4KiB/wg 1 st/lane, 4 wg/CU", "4KiB/wg 1 st/lane, 3 wg/CU",
+        "8KiB/512-thread wg 1 st/lane", "hipMemsetD32Async"};
+    return mode >= 0 && mode < PBK_FILL_SHAPES ? names[mode] : "?";
+}
+
 extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipStream_t st)
 {
     const uint64_t n16 = bytes / 16;
-    const uint32_t per = mode == 2 ? 1 : 4;
-    const uint32_t grid = (uint32_t)((n16 + 256 * per - 1) / (256 * per));
-    if (mode == 0)
-        hipLaunchKernelGGL((pb_fill_kernel<false, 4>), dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
-    else if (mode == 1)
-        hipLaunchKernelGGL((pb_fill_kernel<true, 4>), dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
-    else
-        hipLaunchKernelGGL((pb_fill_kernel<false, 1>), dim3(grid), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+    const uint32_t g4 = (uint32_t)((n16 + 1023) / 1024), g1 = (uint32_t)((n16 + 255) / 256);
+    static const uint32_t cap_lds[4] = {27136u, 32768u, 40960u, 54272u}; // 6, 5, 4, 3 workgroups per CU
+    switch (mode)
+    {
+    case 0:
+        hipLaunchKernelGGL((pb_fill_kernel<false, 4>), dim3(g4), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+        break;
+    case 1:
+        hipLaunchKernelGGL((pb_fill_kernel<true, 4>), dim3(g4), dim3(256), 0, st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+        break;
+    case 2:
+    case 3:
+    case 4:
+    case 5:
+    case 6:
+        hipLaunchKernelGGL((pb_fill_kernel<false, 1>), dim3(g1), dim3(256), mode == 2 ? 0u : cap_lds[mode - 3], st,
+                           (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+        break;
+    case 7:
+        hipLaunchKernelGGL(pb_fill512_kernel, dim3((uint32_t)((n16 + 511) / 512)), dim3(512), 0, st, (pb_u32x4 *)dst,
+                           n16, 0x5A5A5A5Au);
+        break;
+    default:
+        return hipMemsetD32Async((hipDeviceptr_t)dst, 0x5A5A5A5Au, bytes / 4, st);
+    }
     return hipGetLastError();
 }

@@ -128,7 +128,7 @@ class Frames(C.Structure):
     _fields_ = [
         ("data", C.c_void_p),
         ("offsets", C.c_void_p),
-        ("tile_first", C.c_void_p),
+        ("reserved", C.c_void_p),
         ("scan_tmp", C.c_void_p),
         ("capacity_frames", C.c_uint64),
         ("capacity_bytes", C.c_uint64),
@@ -284,7 +284,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pbgpu_kernel_time": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
         "pbgpu_set_timing": (C.c_int, [P, C.c_int]),
         "pbgpu_fill_probe": (C.c_int, [P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
-        "pbgpu_tile_bytes": (C.c_int, [P, C.c_uint16, C.POINTER(C.c_uint32)]),
+        "pbgpu_fill_probe_ex": (C.c_int, [P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+        "pbgpu_fill_shape_name": (C.c_char_p, [C.c_int]),
         "pbgpu_abi_size": (C.c_size_t, [C.c_int]),
         "pbgpu_kernel_name": (C.c_int, [P, C.c_uint16, C.c_char_p, C.c_size_t]),
     }
@@ -424,10 +425,15 @@ class GpuContext:
         _check(self.lib.pbgpu_fill_probe(self.h, nbytes, reps, C.byref(ms)), "fill_probe")
         return float(ms.value)
 
-    def tile_bytes(self, idx: int) -> int:
-        t = C.c_uint32()
-        _check(self.lib.pbgpu_tile_bytes(self.h, idx, C.byref(t)), "tile_bytes")
-        return int(t.value)
+    FILL_SHAPES = 9  # PBGPU_FILL_SHAPES
+
+    def fill_probe_shapes(self, nbytes: int, reps: int):
+        """Every write-probe shape's mean ms per launch {name: ms} and the fastest's name."""
+        ms = (C.c_double * self.FILL_SHAPES)()
+        best = C.c_int()
+        _check(self.lib.pbgpu_fill_probe_ex(self.h, nbytes, reps, ms, C.byref(best)), "fill_probe_ex")
+        names = [self.lib.pbgpu_fill_shape_name(i).decode() for i in range(self.FILL_SHAPES)]
+        return {names[i]: float(ms[i]) for i in range(self.FILL_SHAPES)}, names[best.value]
 
     def kernel_name(self, idx: int) -> str:
         buf = C.create_string_buffer(96)

@@ -1,9 +1,19 @@
-// wbench.hip — HBM write-pattern microbenchmark (gfx950): which store shapes
-// reach the write roofline.  Decides the frame-build kernel's store layout.
+// wbench.hip — HBM write-pattern microbenchmark (gfx950).  Two jobs:
+//  1. the write-roofline denominator: search store shapes (workgroup size,
+//     stores per lane, page ownership, non-temporal, the runtime's memset and
+//     copy paths) for the fastest plain fill of the same bytes;
+//  2. the address-map probe behind the frame kernels' store layout: blocks of G
+//     bytes written at a stride of M blocks (one residue class only) show the
+//     interleave granularity and how many independent units it spreads over, and
+//     a window model (contiguous per-workgroup windows, optional LDS source,
+//     compute delay and occupancy limit) reproduces the staged kernels' store
+//     pattern without their arithmetic.
+// Usage: wbench <bytes> [section ...]   sections: shapes sparse win memset (default: all)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -18,260 +28,470 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         }                                                                            \
     } while (0)
 
-// grid-stride fill, 16 B per lane per iteration
 template <bool NT>
-__global__ __launch_bounds__(256) void fill_gs(u32x4 *dst, uint64_t n16)
+__device__ __forceinline__ void st16(uint8_t *p, u32x4 v)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+    if (NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    else
+        *reinterpret_cast<u32x4 *>(p) = v;
+}
+
+// Page-list fill.  Workgroup b writes `ppw` pages of 2^pgs bytes; its chunk list
+// (ppw * 2^pgs / 16 chunks of 16 B) is dealt to the lanes round robin, so every
+// wave store instruction writes WG*16 contiguous bytes of one page.
+//   mode 0  linear:      page = b * ppw + i
+//   mode 1  XCD-owned:   page = ((b / 8) * ppw + i) * 8 + b % 8   (blocks are dealt to XCDs round robin)
+//   mode 2  XCD pairs:   mode 1 with two adjacent pages per slot (residue classes mod 16 in pairs)
+template <int WG, bool NT>
+__global__ __launch_bounds__(WG) void fill_pages(uint8_t *dst, uint32_t pgs, uint32_t ppw, uint32_t mode)
+{
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint32_t cpp = (1u << pgs) >> 4; // chunks per page
+    const uint32_t nq = ppw * cpp;
+    for (uint32_t q = t; q < nq; q += WG)
     {
-        u32x4 v = {(uint32_t)i, 1u, 2u, 3u};
-        if (NT)
-            __builtin_nontemporal_store(v, dst + i);
+        const uint32_t i = q / cpp, o = (q % cpp) * 16;
+        uint64_t pg;
+        if (mode == 0)
+            pg = (uint64_t)b * ppw + i;
+        else if (mode == 1)
+            pg = ((uint64_t)(b >> 3) * ppw + i) * 8 + (b & 7u);
         else
-            dst[i] = v;
+            pg = (((uint64_t)(b >> 3) * (ppw >> 1) + (i >> 1)) * 8 + (b & 7u)) * 2 + (i & 1u);
+        st16<NT>(dst + (pg << pgs) + o, u32x4{b, q, 2u, 3u});
     }
 }
 
-// one-shot: each thread writes PER 16-B chunks, block covers contiguous 256*PER*16 B
-template <bool NT, int PER>
-__global__ __launch_bounds__(256) void fill_block(uint8_t *dst, uint32_t misalign)
+// Sparse probe: 4 KiB (or one block, if larger) per workgroup, written as blocks
+// of 2^gs bytes at a stride of M blocks, residue `res` only.
+__global__ __launch_bounds__(256) void fill_sparse(uint8_t *dst, uint32_t gs, uint32_t M, uint32_t res)
 {
-    uint8_t *base = dst + (uint64_t)blockIdx.x * 256 * PER * 16 + misalign;
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint32_t per = gs > 12 ? (1u << (gs - 12)) : 1u; // stores per lane
+    const uint64_t wgb = (uint64_t)256 * 16 * per;          // data bytes per workgroup
+    for (uint32_t i = 0; i < per; ++i)
     {
-        u32x4 v = {(uint32_t)blockIdx.x, (uint32_t)i, 2u, 3u};
-        u32x4 *p = (u32x4 *)(base + ((uint64_t)i * 256 + threadIdx.x) * 16);
-        if (NT)
-            __builtin_nontemporal_store(v, p);
-        else
-            *p = v;
+        const uint64_t o = (uint64_t)b * wgb + ((uint64_t)i * 256 + t) * 16; // data offset
+        const uint64_t bi = o >> gs, within = o & ((1ull << gs) - 1);
+        st16<false>(dst + ((bi * M + res) << gs) + within, u32x4{b, i, 2u, 3u});
     }
 }
 
-// frame-per-lane: lane writes 64 contiguous bytes as 4 x 16 B (stride 64 B across lanes)
-template <bool NT>
-__global__ __launch_bounds__(256) void fill_lane64(uint8_t *dst)
+// Window model of the staged kernels' stores: workgroup b writes `nwin` windows
+// of `wb` bytes (a multiple of 16), one after another.  Between windows a
+// dependent VALU chain of `delay` steps stands in for the frame build; with
+// from_lds the chunks are read from LDS (ds_read_b128) and a barrier closes each
+// window, as the kernels do.  Dynamic LDS (launch argument) limits occupancy.
+//   mode 0: the workgroup's region is contiguous (b * nwin * wb)
+//   mode 1: windows are whole 4 KiB pages, XCD-owned as fill_pages mode 1
+__global__ __launch_bounds__(256) void fill_win(uint8_t *dst, uint32_t wb, uint32_t nwin, uint32_t delay,
+                                                uint32_t from_lds, uint32_t mode)
 {
-    uint8_t *base = dst + ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 64;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint32_t nc = wb >> 4;
+    uint32_t x = t * 2654435761u + b;
+    for (uint32_t w = 0; w < nwin; ++w)
     {
-        u32x4 v = {(uint32_t)blockIdx.x, (uint32_t)i, 2u, 3u};
-        if (NT)
-            __builtin_nontemporal_store(v, (u32x4 *)(base + 16 * i));
-        else
-            *(u32x4 *)(base + 16 * i) = v;
-    }
-}
-
-// frame-per-lane through an LDS transpose: lanes write 64 B rows to LDS, then
-// the workgroup streams the 16 KiB tile out with contiguous dwordx4 stores
-template <bool NT>
-__global__ __launch_bounds__(256) void fill_lane64_lds(uint8_t *dst)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t tile[256 * 20]; // 80-B padded rows
-    const uint32_t t = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        *(u32x4 *)(tile + t * 20 + 4 * i) = u32x4{(uint32_t)blockIdx.x, (uint32_t)i, t, 3u};
-    __syncthreads();
-    uint8_t *base = dst + (uint64_t)blockIdx.x * 256 * 64;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-    {
-        const uint32_t c = i * 256 + t; // chunk: frame c / 4, part c % 4
-        u32x4 v = *(const u32x4 *)(tile + (c >> 2) * 20 + 4 * (c & 3));
-        if (NT)
-            __builtin_nontemporal_store(v, (u32x4 *)(base + 16 * c));
-        else
-            *(u32x4 *)(base + 16 * c) = v;
-    }
-}
-
-// dword stores, contiguous per wave (4 B/lane)
-__global__ __launch_bounds__(256) void fill_dword(uint32_t *dst)
-{
-    uint32_t *base = dst + (uint64_t)blockIdx.x * 256 * 16;
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        __builtin_nontemporal_store((uint32_t)i, base + i * 256 + threadIdx.x);
-}
-
-
-// persistent: grid of G blocks; block b writes chunks b, b+G, ... of CH bytes (16 B per lane per store)
-template <int WG, int PER>
-__global__ __launch_bounds__(WG) void fill_chunk(uint8_t *dst, uint64_t nchunks)
-{
-    for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x)
-    {
-        uint8_t *base = dst + c * (uint64_t)WG * PER * 16;
-#pragma unroll
-        for (int i = 0; i < PER; ++i)
+        for (uint32_t d = 0; d < delay; ++d)
+            x = __umul24(x, 1103515245u) + 12345u;
+        if (from_lds)
         {
-            u32x4 v = {(uint32_t)c, (uint32_t)i, 2u, 3u};
-            *(u32x4 *)(base + ((uint64_t)i * WG + threadIdx.x) * 16) = v;
+            for (uint32_t q = t; q < nc; q += 256)
+                reinterpret_cast<u32x4 *>(lds)[q] = u32x4{x, q, w, b};
+            __syncthreads();
+        }
+        for (uint32_t q = t; q < nc; q += 256)
+        {
+            uint64_t a;
+            if (mode == 0)
+                a = ((uint64_t)b * nwin + w) * wb + 16ull * q;
+            else
+            {
+                const uint32_t ppw = wb >> 12;
+                const uint64_t pg = ((uint64_t)(b >> 3) * nwin * ppw + (uint64_t)w * ppw + (q >> 8)) * 8 + (b & 7u);
+                a = (pg << 12) + 16ull * (q & 255u);
+            }
+            const u32x4 v = from_lds ? reinterpret_cast<const u32x4 *>(lds)[q] : u32x4{x, q, w, b};
+            st16<false>(dst + a, v);
+        }
+        if (from_lds)
+            __syncthreads();
+    }
+}
+
+// Window model by workgroup size (from LDS, a barrier per window, linear or
+// XCD-owned pages as fill_win).
+template <int WG>
+__global__ __launch_bounds__(WG) void fill_win2(uint8_t *dst, uint32_t wb, uint32_t nwin, uint32_t mode, uint32_t delay)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint32_t nc = wb >> 4;
+    uint32_t x = t * 2654435761u + b;
+    for (uint32_t w = 0; w < nwin; ++w)
+    {
+        for (uint32_t d = 0; d < delay; ++d)
+            x = __umul24(x, 1103515245u) + 12345u;
+        for (uint32_t q = t; q < nc; q += WG)
+            reinterpret_cast<u32x4 *>(lds)[q] = u32x4{x, q, w, b};
+        __syncthreads();
+        for (uint32_t q = t; q < nc; q += WG)
+        {
+            uint64_t a;
+            if (mode == 0)
+                a = ((uint64_t)b * nwin + w) * wb + 16ull * q;
+            else
+            {
+                const uint32_t ppw = wb >> 12;
+                const uint64_t pg = ((uint64_t)(b >> 3) * nwin * ppw + (uint64_t)w * ppw + (q >> 8)) * 8 + (b & 7u);
+                a = (pg << 12) + 16ull * (q & 255u);
+            }
+            st16<false>(dst + a, reinterpret_cast<const u32x4 *>(lds)[q]);
+        }
+        __syncthreads();
+    }
+}
+
+// Frame-owned pages (the store side of a frame kernel for frames > 128 B):
+// frames of L bytes are packed; a frame owns the 128-B lines from the one holding
+// its first byte up to (not including) the one holding its end, so every line
+// has one writer.  Workgroup b owns `ppw` XCD-strided 4 KiB pages (mode 1) or
+// consecutive pages (mode 0) and writes the lines of every frame whose first line
+// lies in one of its pages: a contiguous range [R(p), R(p + 1)) per page that
+// starts inside page p and may end inside page p + 1.  Lane t stores byte 16 t of
+// each 4 KiB grid page the range touches (1 KiB-aligned wave stores, masked at
+// the range ends).
+__device__ __forceinline__ uint64_t fown_start(uint64_t p, uint32_t L)
+{
+    const uint64_t a = p << 12;
+    uint64_t f = a / L;
+    while (((f * L) & ~127ull) < a)
+        ++f;
+    return (f * L) & ~127ull;
+}
+
+__global__ __launch_bounds__(256) void fill_fown(uint8_t *dst, uint32_t L, uint32_t ppw, uint32_t mode)
+{
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    for (uint32_t i = 0; i < ppw; ++i)
+    {
+        const uint64_t p = mode ? ((uint64_t)(b >> 3) * ppw + i) * 8 + (b & 7u) : (uint64_t)b * ppw + i;
+        const uint64_t r0 = fown_start(p, L), r1 = fown_start(p + 1, L);
+#pragma unroll
+        for (uint32_t g = 0; g < 2; ++g)
+        {
+            const uint64_t a = ((p + g) << 12) + 16ull * t;
+            if (a >= r0 && a < r1)
+                st16<false>(dst + a, u32x4{b, i, g, 3u});
         }
     }
 }
 
-// one-shot blocks of WG threads, PER 16-B stores each
-template <int WG, int PER>
-__global__ __launch_bounds__(WG) void fill_wg(uint8_t *dst)
+// Paced page fill: a dependent chain of d0 24-bit multiply-adds before the first
+// page and d1 before each further one (standing in for frame arithmetic), with
+// dynamic LDS limiting the workgroups per CU.  fill_pages' page maps (mode 0/1).
+__global__ __launch_bounds__(256) void fill_paced(uint8_t *dst, uint32_t ppw, uint32_t mode, uint32_t d0, uint32_t d1)
 {
-    uint8_t *base = dst + (uint64_t)blockIdx.x * WG * PER * 16;
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
+    extern __shared__ uint32_t lds_dummy[];
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    uint32_t x = t * 2654435761u + b;
+    for (uint32_t d = 0; d < d0; ++d)
+        x = __umul24(x, 1103515245u) + 12345u;
+    for (uint32_t i = 0; i < ppw; ++i)
     {
-        u32x4 v = {(uint32_t)blockIdx.x, (uint32_t)i, 2u, 3u};
-        *(u32x4 *)(base + ((uint64_t)i * WG + threadIdx.x) * 16) = v;
+        if (i)
+            for (uint32_t d = 0; d < d1; ++d)
+                x = __umul24(x, 1103515245u) + 12345u;
+        const uint64_t pg = mode ? ((uint64_t)(b >> 3) * ppw + i) * 8 + (b & 7u) : (uint64_t)b * ppw + i;
+        st16<false>(dst + (pg << 12) + 16 * t, u32x4{x, i, 2u, 3u});
+    }
+    if (x == 0x12345678u && t == 999) // keep the chain
+        lds_dummy[0] = x;
+}
+
+// Strided page ownership: workgroup b writes `ppw` 4 KiB pages at a stride of S
+// pages, page = ((b / S) * ppw + i) * S + b % S (S = 1: linear 4*ppw KiB; S = 8:
+// the XCD-owned layout).  Separates "8 XCDs own 8 residues" from "concurrent
+// pages of one workgroup far apart".
+__global__ __launch_bounds__(256) void fill_stride(uint8_t *dst, uint32_t ppw, uint32_t S)
+{
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    for (uint32_t i = 0; i < ppw; ++i)
+    {
+        const uint64_t pg = ((uint64_t)(b / S) * ppw + i) * S + (b % S);
+        st16<false>(dst + (pg << 12) + 16 * t, u32x4{b, i, 2u, 3u});
     }
 }
 
-// one-shot blocks, wave-major order: wave w writes its own contiguous PER KiB
-template <int WG, int PER>
-__global__ __launch_bounds__(WG) void fill_wave(uint8_t *dst)
-{
-    const uint32_t w = threadIdx.x / 64, l = threadIdx.x % 64;
-    uint8_t *base = dst + (uint64_t)blockIdx.x * WG * PER * 16 + (uint64_t)w * PER * 1024;
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-    {
-        u32x4 v = {(uint32_t)blockIdx.x, (uint32_t)i, 2u, 3u};
-        *(u32x4 *)(base + ((uint64_t)i * 64 + l) * 16) = v;
-    }
-}
-
-// XCD-aware: block b (dealt to XCD b % 8) writes PER chunks of CH bytes, chunk index ((b/8)*PER + i)*8 + (b+ROT)%8
-template <int WG, int PER, int CH, int ROT>
-__global__ __launch_bounds__(WG) void fill_xcd(uint8_t *dst)
-{
-    const uint32_t b = blockIdx.x;
-    constexpr int SPC = CH / (WG * 16); // stores per chunk per lane
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-    {
-        const uint64_t c = ((uint64_t)(b >> 3) * PER + i) * 8 + ((b + ROT) & 7);
-#pragma unroll
-        for (int s = 0; s < SPC; ++s)
-        {
-            u32x4 v = {b, (uint32_t)i, 2u, 3u};
-            *(u32x4 *)(dst + c * CH + ((uint64_t)s * WG + threadIdx.x) * 16) = v;
-        }
-    }
-}
-
-// XCD-aware with arbitrary chunk bytes CB (multiple of 16, <= WG*16*SPC): chunk c at c*CB + off
-template <int WG, int PER, int SPC>
-__global__ __launch_bounds__(WG) void fill_xcdb(uint8_t *dst, uint32_t CB, uint32_t off)
-{
-    const uint32_t b = blockIdx.x;
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-    {
-        const uint64_t c = ((uint64_t)(b >> 3) * PER + i) * 8 + (b & 7);
-#pragma unroll
-        for (int s = 0; s < SPC; ++s)
-        {
-            const uint32_t o = (s * WG + threadIdx.x) * 16;
-            u32x4 v = {b, (uint32_t)i, 2u, 3u};
-            if (o < CB)
-                *(u32x4 *)(dst + off + c * CB + o) = v;
-        }
-    }
-}
-
+// Kernel timing: best of 3 trials, each the mean of `reps` back-to-back launches
+// after one untimed launch.
 template <typename F>
 double timeit(F launch, int reps)
 {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    launch();
-    CK(hipDeviceSynchronize());
-    CK(hipEventRecord(a));
-    for (int r = 0; r < reps; ++r)
+    double best = 1e30;
+    for (int trial = 0; trial < 3; ++trial)
+    {
         launch();
-    CK(hipEventRecord(b));
-    CK(hipEventSynchronize(b));
-    float ms;
-    CK(hipEventElapsedTime(&ms, a, b));
-    return ms / reps;
+        CK(hipEventRecord(a));
+        for (int r = 0; r < reps; ++r)
+            launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (ms / reps < best)
+            best = ms / reps;
+    }
+    CK(hipGetLastError());
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+    return best;
+}
+
+static uint64_t g_bytes;
+static void rep(const char *name, uint64_t bytes, double ms)
+{
+    printf("%-56s %9.4f ms %9.1f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+}
+
+template <int WG, bool NT>
+static void pages_case(uint8_t *buf, uint32_t pgs, uint32_t ppw, uint32_t mode)
+{
+    const uint64_t pgb = 1ull << pgs;
+    const uint64_t wgbytes = pgb * ppw;
+    const uint32_t grid = (uint32_t)(g_bytes / wgbytes / 8 * 8); // whole XCD rounds
+    const uint64_t bytes = (uint64_t)grid * wgbytes;
+    char nm[96];
+    static const char *mn[] = {"linear", "xcd", "xcd-pair"};
+    snprintf(nm, sizeof nm, "pages %s wg=%d page=%llu ppw=%u st/lane=%llu%s", mn[mode], WG,
+             (unsigned long long)pgb, ppw, (unsigned long long)(wgbytes / 16 / WG), NT ? " nt" : "");
+    rep(nm, bytes, timeit([&] { hipLaunchKernelGGL((fill_pages<WG, NT>), dim3(grid), dim3(WG), 0, 0, buf, pgs, ppw, mode); }, 20));
+}
+
+static bool want(int argc, char **argv, const char *s)
+{
+    if (argc <= 2)
+        return true;
+    for (int i = 2; i < argc; ++i)
+        if (!strcmp(argv[i], s))
+            return true;
+    return false;
 }
 
 int main(int argc, char **argv)
 {
-    const uint64_t bytes = (argc > 1 ? strtoull(argv[1], 0, 0) : (4ull << 30));
+    g_bytes = (argc > 1 ? strtoull(argv[1], 0, 0) : (2ull << 30));
+    const uint64_t sparse_data = g_bytes / 2 < (1ull << 30) ? g_bytes / 2 : (1ull << 30);
+    const uint64_t alloc = 2 * g_bytes + 8192 > 32 * sparse_data + (1 << 20) ? 2 * g_bytes + 8192 : 32 * sparse_data + (1 << 20); // sparse strides up to 32 blocks
     uint8_t *buf;
-    CK(hipMalloc(&buf, bytes + 4096));
-    const int reps = 20;
-    auto rep = [&](const char *name, double ms) {
-        printf("%-40s %8.3f ms  %8.1f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
-    };
-    if (argc > 2)
+    CK(hipMalloc(&buf, alloc));
+    CK(hipMemset(buf, 0, alloc));
+    CK(hipDeviceSynchronize());
+    printf("# wbench: %llu bytes per fill\n", (unsigned long long)g_bytes);
+
+    if (want(argc, argv, "shapes"))
     {
-        // size / shape sweep of plain 16-B stores (argv[2] = any): which shape and buffer size reach the write ceiling
-#define WG_CASE(WG, PER)                                                                                           \
-    {                                                                                                              \
-        char nm[64];                                                                                               \
-        snprintf(nm, 64, "wg=%d per=%d", WG, PER);                                                                 \
-        rep(nm, timeit([&] { hipLaunchKernelGGL((fill_wg<WG, PER>), dim3(bytes / (WG * PER * 16)), dim3(WG), 0, 0, buf); }, reps)); \
+        // one store per lane per 4 KiB page, every workgroup size; 2 / 4 stores per lane
+        pages_case<64, false>(buf, 10, 1, 0);   // 1 KiB per 64-thread workgroup
+        pages_case<64, false>(buf, 12, 1, 0);   // 4 KiB per 64-thread workgroup (4 stores / lane)
+        pages_case<128, false>(buf, 11, 1, 0);  // 2 KiB per 128-thread workgroup
+        pages_case<128, false>(buf, 12, 1, 0);  // 4 KiB per 128-thread workgroup (2 / lane)
+        pages_case<256, false>(buf, 12, 1, 0);  // the round-1 best shape
+        pages_case<256, false>(buf, 13, 1, 0);  // 8 KiB per workgroup (2 / lane)
+        pages_case<256, false>(buf, 12, 2, 0);
+        pages_case<256, false>(buf, 12, 4, 0);
+        pages_case<512, false>(buf, 13, 1, 0);  // 8 KiB per 512-thread workgroup (1 / lane)
+        pages_case<512, false>(buf, 12, 2, 0);
+        pages_case<1024, false>(buf, 14, 1, 0); // 16 KiB per 1024-thread workgroup (1 / lane)
+        pages_case<1024, false>(buf, 12, 4, 0);
+        // XCD-owned 4 KiB pages
+        pages_case<64, false>(buf, 12, 1, 1);
+        pages_case<64, false>(buf, 12, 4, 1);
+        pages_case<128, false>(buf, 12, 2, 1);
+        pages_case<256, false>(buf, 12, 1, 1);
+        pages_case<256, false>(buf, 12, 2, 1);
+        pages_case<256, false>(buf, 12, 4, 1);
+        pages_case<256, false>(buf, 12, 8, 1);
+        pages_case<256, false>(buf, 12, 16, 1);
+        pages_case<512, false>(buf, 12, 2, 1);
+        pages_case<512, false>(buf, 12, 8, 1);
+        pages_case<1024, false>(buf, 12, 4, 1);
+        pages_case<1024, false>(buf, 12, 16, 1);
+        pages_case<256, false>(buf, 12, 4, 2);
+        pages_case<256, false>(buf, 11, 4, 1); // 2 KiB pages, XCD-owned
+        pages_case<256, false>(buf, 13, 2, 1); // 8 KiB pages, XCD-owned
+        // non-temporal
+        pages_case<256, true>(buf, 12, 1, 0);
+        pages_case<256, true>(buf, 12, 4, 1);
+        pages_case<1024, true>(buf, 14, 1, 0);
     }
-        WG_CASE(256, 1) WG_CASE(256, 4)
-#define XC_CASE(WG, PER, CH, ROT)                                                                                  \
-    {                                                                                                              \
-        char nm[64];                                                                                               \
-        snprintf(nm, 64, "xcd wg=%d per=%d ch=%d rot=%d", WG, PER, CH, ROT);                                        \
-        rep(nm, timeit([&] { hipLaunchKernelGGL((fill_xcd<WG, PER, CH, ROT>), dim3(bytes / ((uint64_t)PER * CH)), dim3(WG), 0, 0, buf); }, reps)); \
-    }
-        XC_CASE(256, 4, 4096, 0)
-#define XB_CASE(WG, PER, SPC, CB, OFF)                                                                             \
-    {                                                                                                              \
-        char nm[64];                                                                                               \
-        snprintf(nm, 64, "xcdb wg=%d per=%d cb=%d off=%d", WG, PER, CB, OFF);                                      \
-        rep(nm, timeit([&] { hipLaunchKernelGGL((fill_xcdb<WG, PER, SPC>), dim3((bytes - 65536) / ((uint64_t)PER * CB)), dim3(WG), 0, 0, buf, (uint32_t)CB, (uint32_t)OFF); }, reps)); \
-    }
-        XB_CASE(256, 4, 1, 4096, 0) XB_CASE(256, 4, 1, 4096, 256) XB_CASE(256, 4, 1, 4096, 1024) XB_CASE(256, 4, 1, 4096, 2048)
-        XB_CASE(256, 4, 1, 3840, 0) XB_CASE(256, 4, 1, 3584, 0) XB_CASE(256, 4, 2, 6144, 0) XB_CASE(256, 4, 2, 5120, 0)
-        XB_CASE(256, 1, 1, 3840, 0) XB_CASE(256, 1, 1, 4096, 2048) XB_CASE(256, 1, 2, 6000, 0) XB_CASE(256, 2, 2, 6000, 0)
-        XB_CASE(256, 1, 4, 12288, 0) XB_CASE(256, 2, 4, 12288, 0) XB_CASE(256, 1, 4, 16384, 0)
-#define CH_CASE(WG, PER, G)                                                                                        \
-    {                                                                                                              \
-        char nm[64];                                                                                               \
-        snprintf(nm, 64, "persistent wg=%d per=%d grid=%d", WG, PER, G);                                           \
-        rep(nm, timeit([&] { hipLaunchKernelGGL((fill_chunk<WG, PER>), dim3(G), dim3(WG), 0, 0, buf, bytes / (WG * PER * 16)); }, reps)); \
-    }
-        CH_CASE(1024, 8, 256)
-        CK(hipFree(buf));
-        return 0;
-    }
-    const uint64_t n16 = bytes / 16;
-    for (int g : {1024, 2048, 4096, 8192, 16384, 65536})
+    if (want(argc, argv, "win2"))
     {
-        char nm[64];
-        snprintf(nm, 64, "grid-stride nt grid=%d", g);
-        rep(nm, timeit([&] { hipLaunchKernelGGL(fill_gs<true>, dim3(g), dim3(256), 0, 0, (u32x4 *)buf, n16); },
-                       reps));
-        snprintf(nm, 64, "grid-stride plain grid=%d", g);
-        rep(nm, timeit([&] { hipLaunchKernelGGL(fill_gs<false>, dim3(g), dim3(256), 0, 0, (u32x4 *)buf, n16); },
-                       reps));
+        struct W
+        {
+            int wg;
+            uint32_t wb, nwin, lds, mode, delay;
+        } cases[] = {
+            {1024, 16384, 1, 16384, 0, 0},   {1024, 24576, 1, 24576, 0, 0},  {1024, 32768, 1, 32768, 0, 0},
+            {1024, 49152, 1, 49152, 0, 0},   {1024, 65536, 1, 65536, 0, 0},  {1024, 98304, 1, 98304, 0, 0},
+            {512, 8192, 1, 8192, 0, 0},      {512, 16384, 1, 16384, 0, 0},   {512, 24576, 1, 24576, 0, 0},
+            {512, 49152, 1, 49152, 0, 0},    {256, 8192, 1, 8192, 0, 0},     {256, 16384, 1, 16384, 0, 0},
+            {1024, 49152, 1, 49152, 0, 300}, {1024, 49152, 1, 49152, 0, 1500}, {1024, 16384, 1, 16384, 0, 1500},
+            {512, 24576, 1, 24576, 0, 1500}, {1024, 49152, 1, 49152, 1, 0},  {1024, 49152, 1, 49152, 1, 1500},
+            {1024, 98304, 1, 98304, 1, 0},   {1024, 49152, 2, 49152, 0, 0},
+        };
+        for (const W &c : cases)
+        {
+            const uint64_t wgbytes = (uint64_t)c.wb * c.nwin;
+            const uint32_t grid = (uint32_t)(g_bytes / wgbytes / 8 * 8);
+            char nm[128];
+            snprintf(nm, sizeof nm, "win2 %s wg=%d wb=%u nwin=%u lds=%u delay=%u st/lane/win=%.1f", c.mode ? "xcd" : "linear",
+                     c.wg, c.wb, c.nwin, c.lds, c.delay, c.wb / 16.0 / c.wg);
+            auto L = [&] {
+                if (c.wg == 256)
+                    hipLaunchKernelGGL(fill_win2<256>, dim3(grid), dim3(256), c.lds, 0, buf, c.wb, c.nwin, c.mode, c.delay);
+                else if (c.wg == 512)
+                    hipLaunchKernelGGL(fill_win2<512>, dim3(grid), dim3(512), c.lds, 0, buf, c.wb, c.nwin, c.mode, c.delay);
+                else
+                    hipLaunchKernelGGL(fill_win2<1024>, dim3(grid), dim3(1024), c.lds, 0, buf, c.wb, c.nwin, c.mode, c.delay);
+            };
+            rep(nm, (uint64_t)grid * wgbytes, timeit(L, 10));
+        }
     }
-    const uint32_t nb4 = (uint32_t)(bytes / (256 * 4 * 16));
-    const uint32_t nb16 = (uint32_t)(bytes / (256 * 16 * 16));
-    rep("block PER=4 nt aligned", timeit([&] { hipLaunchKernelGGL((fill_block<true, 4>), dim3(nb4), dim3(256), 0, 0, buf, 0u); }, reps));
-    rep("block PER=4 plain aligned", timeit([&] { hipLaunchKernelGGL((fill_block<false, 4>), dim3(nb4), dim3(256), 0, 0, buf, 0u); }, reps));
-    rep("block PER=16 nt aligned", timeit([&] { hipLaunchKernelGGL((fill_block<true, 16>), dim3(nb16), dim3(256), 0, 0, buf, 0u); }, reps));
-    rep("block PER=16 plain aligned", timeit([&] { hipLaunchKernelGGL((fill_block<false, 16>), dim3(nb16), dim3(256), 0, 0, buf, 0u); }, reps));
-    rep("block PER=4 nt misalign 4", timeit([&] { hipLaunchKernelGGL((fill_block<true, 4>), dim3(nb4), dim3(256), 0, 0, buf, 4u); }, reps));
-    rep("block PER=4 nt misalign 2", timeit([&] { hipLaunchKernelGGL((fill_block<true, 4>), dim3(nb4), dim3(256), 0, 0, buf, 2u); }, reps));
-    rep("block PER=4 nt misalign 1", timeit([&] { hipLaunchKernelGGL((fill_block<true, 4>), dim3(nb4), dim3(256), 0, 0, buf, 1u); }, reps));
-    rep("block PER=4 plain misalign 4", timeit([&] { hipLaunchKernelGGL((fill_block<false, 4>), dim3(nb4), dim3(256), 0, 0, buf, 4u); }, reps));
-    rep("lane64 nt (4x16B, 64B lane stride)", timeit([&] { hipLaunchKernelGGL(fill_lane64<true>, dim3(nb4), dim3(256), 0, 0, buf); }, reps));
-    rep("lane64 plain", timeit([&] { hipLaunchKernelGGL(fill_lane64<false>, dim3(nb4), dim3(256), 0, 0, buf); }, reps));
-    rep("lane64 via LDS nt", timeit([&] { hipLaunchKernelGGL(fill_lane64_lds<true>, dim3(nb4), dim3(256), 0, 0, buf); }, reps));
-    rep("lane64 via LDS plain", timeit([&] { hipLaunchKernelGGL(fill_lane64_lds<false>, dim3(nb4), dim3(256), 0, 0, buf); }, reps));
-    rep("dword nt contiguous", timeit([&] { hipLaunchKernelGGL(fill_dword, dim3(nb16), dim3(256), 0, 0, (uint32_t *)buf); }, reps));
+    if (want(argc, argv, "fown"))
+    {
+        for (uint32_t L : {1500u, 1024u, 824u, 4096u})
+            for (uint32_t mode : {0u, 1u})
+                for (uint32_t ppw : {1u, 4u, 8u})
+                {
+                    const uint32_t grid = (uint32_t)((g_bytes - 65536) / (4096ull * ppw) / 8 * 8);
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "fown %s L=%u pages/wg=%u", mode ? "xcd" : "linear", L, ppw);
+                    rep(nm, (uint64_t)grid * 4096 * ppw,
+                        timeit([&] { hipLaunchKernelGGL(fill_fown, dim3(grid), dim3(256), 0, 0, buf, L, ppw, mode); }, 20));
+                }
+    }
+    if (want(argc, argv, "paced"))
+    {
+        struct P
+        {
+            uint32_t ppw, mode, d0, d1, lds;
+        } cases[] = {
+            {1, 0, 0, 0, 0},    {1, 0, 8, 0, 0},    {1, 0, 16, 0, 0},   {1, 0, 32, 0, 0},   {1, 0, 64, 0, 0},
+            {1, 0, 128, 0, 0},  {1, 0, 256, 0, 0},  {1, 1, 0, 0, 0},    {1, 1, 32, 0, 0},   {1, 1, 128, 0, 0},
+            {4, 1, 0, 0, 0},    {4, 1, 32, 0, 0},   {4, 1, 32, 32, 0},  {4, 1, 128, 128, 0}, {4, 0, 32, 32, 0},
+            {4, 0, 128, 128, 0}, {8, 1, 64, 64, 0}, {16, 1, 64, 64, 0}, {1, 0, 0, 0, 40960}, {1, 0, 0, 0, 81920},
+            {1, 0, 32, 0, 40960}, {4, 1, 32, 32, 40960}, {4, 1, 32, 32, 81920},
+        };
+        for (const P &c : cases)
+        {
+            const uint32_t grid = (uint32_t)(g_bytes / (4096ull * c.ppw) / 8 * 8);
+            char nm[96];
+            snprintf(nm, sizeof nm, "paced %s pages/wg=%u d0=%u d1=%u lds=%u", c.mode ? "xcd" : "linear", c.ppw, c.d0, c.d1,
+                     c.lds);
+            rep(nm, (uint64_t)grid * 4096 * c.ppw,
+                timeit([&] { hipLaunchKernelGGL(fill_paced, dim3(grid), dim3(256), c.lds, 0, buf, c.ppw, c.mode, c.d0, c.d1); }, 20));
+        }
+    }
+    if (want(argc, argv, "occ"))
+    {
+        // workgroups per CU limited by dynamic LDS: 8 (none), 6, 5, 4, 3, 2 of 256 threads
+        const uint32_t ldsv[] = {0u, 24576u, 30720u, 40960u, 53248u, 81920u};
+        for (uint32_t mode : {0u, 1u})
+            for (uint32_t ppw : {1u, 4u})
+                for (uint32_t lds : ldsv)
+                {
+                    const uint32_t grid = (uint32_t)(g_bytes / (4096ull * ppw) / 8 * 8);
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "occ %s pages/wg=%u lds=%u (wg/cu=%u)", mode ? "xcd" : "linear", ppw, lds,
+                             lds ? (163840u / lds < 8 ? 163840u / lds : 8u) : 8u);
+                    rep(nm, (uint64_t)grid * 4096 * ppw,
+                        timeit([&] { hipLaunchKernelGGL(fill_paced, dim3(grid), dim3(256), lds, 0, buf, ppw, mode, 0u, 0u); }, 20));
+                }
+        for (uint32_t mode : {0u, 1u})
+            for (uint32_t lds : ldsv)
+            {
+                if (lds && lds < 24576)
+                    continue;
+                const uint32_t wb = 24576, nwin = 4;
+                const uint32_t l = lds ? lds : 24576;
+                const uint32_t grid = (uint32_t)(g_bytes / ((uint64_t)wb * nwin) / 8 * 8);
+                char nm[96];
+                snprintf(nm, sizeof nm, "occ win %s wb=24576 nwin=4 from-lds lds=%u", mode ? "xcd" : "linear", l);
+                rep(nm, (uint64_t)grid * wb * nwin,
+                    timeit([&] { hipLaunchKernelGGL(fill_win, dim3(grid), dim3(256), l, 0, buf, wb, nwin, 0u, 1u, mode); }, 10));
+            }
+    }
+    if (want(argc, argv, "stride"))
+    {
+        for (uint32_t ppw : {2u, 4u, 8u})
+            for (uint32_t S : {1u, 2u, 4u, 8u, 16u, 32u, 64u, 128u, 7u, 9u})
+            {
+                const uint32_t grid = (uint32_t)(g_bytes / (4096ull * ppw) / (8 * S) * (8 * S));
+                char nm[96];
+                snprintf(nm, sizeof nm, "stride pages=%u stride=%u", ppw, S);
+                rep(nm, (uint64_t)grid * 4096 * ppw,
+                    timeit([&] { hipLaunchKernelGGL(fill_stride, dim3(grid), dim3(256), 0, 0, buf, ppw, S); }, 20));
+            }
+    }
+    if (want(argc, argv, "memset"))
+    {
+        rep("hipMemsetD32Async", g_bytes,
+            timeit([&] { CK(hipMemsetD32Async((hipDeviceptr_t)buf, 0x5EEDBA5Eu, g_bytes / 4, 0)); }, 20));
+        rep("hipMemsetAsync (bytes)", g_bytes, timeit([&] { CK(hipMemsetAsync(buf, 0x5E, g_bytes, 0)); }, 20));
+        // a device-to-device copy writes g_bytes (and reads as many)
+        rep("hipMemcpyAsync D2D (bytes written)", g_bytes,
+            timeit([&] { CK(hipMemcpyAsync(buf, buf + g_bytes + 4096, g_bytes, hipMemcpyDeviceToDevice, 0)); }, 20));
+    }
+    if (want(argc, argv, "sparse"))
+    {
+        // G bytes at a stride of M blocks: the interleave granularity and its width
+        const uint64_t data = sparse_data;
+        for (uint32_t gs : {8u, 10u, 12u, 13u, 14u})
+            for (uint32_t M : {1u, 2u, 4u, 8u, 16u, 32u})
+            {
+                const uint32_t per = gs > 12 ? (1u << (gs - 12)) : 1u;
+                const uint32_t grid = (uint32_t)(data / (4096ull * per));
+                char nm[96];
+                snprintf(nm, sizeof nm, "sparse block=%u stride=%u blocks (residue 0)", 1u << gs, M);
+                rep(nm, (uint64_t)grid * 4096 * per,
+                    timeit([&] { hipLaunchKernelGGL(fill_sparse, dim3(grid), dim3(256), 0, 0, buf, gs, M, 0u); }, 10));
+            }
+    }
+    if (want(argc, argv, "win"))
+    {
+        // the staged kernels' store pattern without their arithmetic
+        struct W
+        {
+            uint32_t wb, nwin, delay, from_lds, lds, mode;
+        } cases[] = {
+            {24576, 4, 0, 0, 0, 0},     {24576, 4, 0, 1, 24576, 0}, {24576, 4, 0, 1, 30720, 0},
+            {24576, 4, 200, 1, 30720, 0}, {24576, 1, 0, 1, 30720, 0}, {24576, 16, 0, 1, 30720, 0},
+            {24576, 4, 0, 1, 30720, 1}, {24576, 4, 200, 1, 30720, 1}, {24576, 1, 0, 1, 30720, 1},
+            {4096, 24, 0, 1, 30720, 1}, {4096, 24, 0, 1, 30720, 0},  {16384, 6, 0, 1, 30720, 1},
+            {16384, 6, 0, 1, 20480, 1}, {16384, 6, 0, 1, 16384, 0},
+        };
+        for (const W &c : cases)
+        {
+            const uint64_t wgbytes = (uint64_t)c.wb * c.nwin;
+            const uint32_t grid = (uint32_t)(g_bytes / wgbytes / 8 * 8);
+            char nm[128];
+            snprintf(nm, sizeof nm, "win %s wb=%u nwin=%u delay=%u lds=%u%s", c.mode ? "xcd" : "linear", c.wb, c.nwin,
+                     c.delay, c.lds, c.from_lds ? " from-lds" : "");
+            rep(nm, (uint64_t)grid * wgbytes,
+                timeit([&] {
+                    hipLaunchKernelGGL(fill_win, dim3(grid), dim3(256), c.lds, 0, buf, c.wb, c.nwin, c.delay, c.from_lds,
+                                       c.mode);
+                },
+                       10));
+        }
+    }
     CK(hipFree(buf));
     return 0;
 }

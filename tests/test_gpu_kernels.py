@@ -25,7 +25,6 @@ SHAPES = [
       "pb_vstage_kernel")),
     ("linear_small", {"PBGPU_KERNEL": "linear"},
      ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel")),
-    ("tile", {"PBGPU_KERNEL": "tile"}, ("pb_build_kernel",)),
     ("stage_g8_wgf5", {"PBGPU_KERNEL": "stage", "PBGPU_G": "8", "PBGPU_WGF": "5"},
      ("pb_stage_kernel<8", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("stage_g64_kb4", {"PBGPU_KERNEL": "stage", "PBGPU_G": "64", "PBGPU_STAGE_KB": "4"},
