@@ -60,7 +60,7 @@ typedef struct pbgpu_frames
 {
     uint8_t *data;          /* device pointer, capacity_bytes (16-B padded) */
     uint64_t *offsets;      /* device pointer, capacity_frames + 1 entries */
-    void *reserved;         /* unused (keeps the layout of earlier builds) */
+    void *reserved;         /* library-internal: the buffer's build-completion event */
     uint64_t *scan_tmp;     /* device scratch (length scan) */
     uint64_t capacity_frames;
     uint64_t capacity_bytes;
@@ -112,7 +112,11 @@ int pbgpu_copy_packed(pbgpu_ctx *ctx, const pbgpu_frames *frames, void *host_dst
 int pbgpu_copy_offsets(pbgpu_ctx *ctx, const pbgpu_frames *frames, uint64_t *host_dst);
 /* UMEM landing (af_xdp.c:200-214 geometry): frame first_frame + j lands at
  * umem + (first_slot + j) * slot_stride; lens_out[j] = its length.  `umem`
- * may be any host pointer; pbgpu_host_register() it first for full speed. */
+ * may be any host pointer; pbgpu_host_register() it first for full speed.
+ * Runs on the context's landing stream after the build of `frames` only, so a
+ * build of another buffer queued meanwhile overlaps it (double buffering);
+ * returns when the frames are in place.  A frame longer than slot_stride is
+ * refused (-EINVAL). */
 int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *frames, void *umem, uint32_t slot_stride,
                        uint32_t first_slot, uint64_t first_frame, uint32_t n, uint16_t *lens_out);
 int pbgpu_host_register(pbgpu_ctx *ctx, void *ptr, size_t bytes);

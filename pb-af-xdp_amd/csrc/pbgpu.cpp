@@ -91,7 +91,9 @@ struct timing_pair
 struct pbgpu_ctx
 {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // frame builds
+    hipStream_t land_stream = nullptr; // UMEM landing: overlaps the next build (pbgpu_copy_to_umem)
+    bool land_events = false;          // set by the first landing: builds then record a completion event
     uint2 *d_jump = nullptr;
     uint2 *d_lcg48 = nullptr;
     unsigned long long *d_dbg = nullptr; // PBGPU_TIMING: per-workgroup phase stamps
@@ -340,8 +342,11 @@ int pbgpu_open(int device, pbgpu_ctx **out)
     HIPCHK(hipSetDevice(device));
     pbgpu_ctx *ctx = new pbgpu_ctx();
     ctx->device = device;
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->land_stream, hipStreamNonBlocking) != hipSuccess)
     {
+        if (ctx->stream)
+            (void)hipStreamDestroy(ctx->stream);
         delete ctx;
         return PBGPU_EIO;
     }
@@ -378,6 +383,8 @@ void pbgpu_close(pbgpu_ctx *ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream)
         (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->land_stream)
+        (void)hipStreamSynchronize(ctx->land_stream);
     for (auto &s : ctx->seqs)
         slot_free(s);
     for (auto &p : ctx->pending)
@@ -408,6 +415,8 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipHostFree(ctx->h_lens);
     if (ctx->stream)
         (void)hipStreamDestroy(ctx->stream);
+    if (ctx->land_stream)
+        (void)hipStreamDestroy(ctx->land_stream);
     delete ctx;
 }
 
@@ -937,7 +946,10 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
     {
         (void)hipSetDevice(ctx->device);
         (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamSynchronize(ctx->land_stream);
     }
+    if (f->reserved)
+        (void)hipEventDestroy((hipEvent_t)f->reserved);
     if (f->data)
         (void)hipFree(f->data);
     if (f->offsets)
@@ -991,6 +1003,24 @@ static void report_phase_timing(pbgpu_ctx *ctx, uint64_t n_wg)
             "\"cycles_S_sum\": %.0f, \"life_us\": %.3f, \"span_us\": %.3f, \"resident_wg\": %.1f}}\n",
             (unsigned long long)n, ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, life / n / 100.0, (t1 - t0) / 100.0,
             life / (double)(t1 - t0));
+}
+
+// The frames' build-completion event (kept in pbgpu_frames.reserved): the
+// landing stream waits on it, so landing one buffer overlaps building the next.
+static int mark_built(pbgpu_ctx *ctx, pbgpu_frames *out)
+{
+    // only for callers that land frames: an event record per launch would cost a
+    // release between back-to-back builds that are never landed (bench)
+    if (!ctx->land_events)
+        return PBGPU_OK;
+    if (out->reserved == NULL)
+    {
+        hipEvent_t ev;
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        out->reserved = (void *)ev;
+    }
+    HIPCHK(hipEventRecord((hipEvent_t)out->reserved, ctx->stream));
+    return PBGPU_OK;
 }
 
 int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, pbgpu_frames *out)
@@ -1082,11 +1112,13 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         }
         HIPCHK(pbk_launch_build(&K, ctx->stream));
         ++ctx->span_n;
-        return PBGPU_OK;
+        return mark_built(ctx, out);
     }
     HIPCHK(hipEventRecord(tp.a, ctx->stream));
     HIPCHK(pbk_launch_build(&K, ctx->stream));
     HIPCHK(hipEventRecord(tp.b, ctx->stream));
+    if ((rc = mark_built(ctx, out)) != PBGPU_OK)
+        return rc;
     if (timing)
         report_phase_timing(ctx, n_wg);
     ctx->pending.push_back(tp);
@@ -1184,6 +1216,14 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
     if (n == 0)
         return PBGPU_OK;
     HIPCHK(hipSetDevice(ctx->device));
+    // the landing stream waits for the build of these frames only: a build queued
+    // after it (the caller's next batch) keeps running meanwhile
+    hipStream_t ls = ctx->land_stream;
+    ctx->land_events = true;
+    if (f->reserved)
+        HIPCHK(hipStreamWaitEvent(ls, (hipEvent_t)f->reserved, 0));
+    else
+        HIPCHK(hipStreamSynchronize(ctx->stream));
     uint8_t *dst = (uint8_t *)umem + (uint64_t)first_slot * slot_stride;
     if (f->fixed_len)
     {
@@ -1195,14 +1235,14 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
         if (hipHostGetDevicePointer(&dev_dst, dst, 0) == hipSuccess && dev_dst != NULL &&
             !getenv("PBGPU_UMEM_DMA"))
             HIPCHK(pbk_launch_scatter_fixed(f->data + first_frame * f->fixed_len, f->fixed_len, n, (uint8_t *)dev_dst,
-                                            slot_stride, ctx->stream));
+                                            slot_stride, ls));
         else
         {
             (void)hipGetLastError();
             HIPCHK(hipMemcpy2DAsync(dst, slot_stride, f->data + first_frame * f->fixed_len, f->fixed_len,
-                                    f->fixed_len, n, hipMemcpyDeviceToHost, ctx->stream));
+                                    f->fixed_len, n, hipMemcpyDeviceToHost, ls));
         }
-        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipStreamSynchronize(ls));
         if (lens_out)
             for (uint32_t i = 0; i < n; ++i)
                 lens_out[i] = (uint16_t)f->fixed_len;
@@ -1226,7 +1266,7 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
         // never through a stream-ordered allocation or a pageable async copy
         if (ctx->lens_cap < n)
         {
-            HIPCHK(hipStreamSynchronize(ctx->stream));
+            HIPCHK(hipStreamSynchronize(ls));
             if (ctx->d_lens)
                 (void)hipFree(ctx->d_lens);
             if (ctx->h_lens)
@@ -1240,9 +1280,9 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
         }
         d_lens = ctx->d_lens;
         HIPCHK(pbk_launch_scatter(f->data, f->offsets, first_frame, n, (uint8_t *)dev_dst, slot_stride, d_lens,
-                                  ctx->stream));
-        HIPCHK(hipMemcpyAsync(ctx->h_lens, d_lens, (size_t)n * 2, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
+                                  ls));
+        HIPCHK(hipMemcpyAsync(ctx->h_lens, d_lens, (size_t)n * 2, hipMemcpyDeviceToHost, ls));
+        HIPCHK(hipStreamSynchronize(ls));
         if (lens_out)
             memcpy(lens_out, ctx->h_lens, (size_t)n * 2);
         return PBGPU_OK;
@@ -1250,8 +1290,8 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
     (void)hipGetLastError();
     std::vector<uint64_t> off(n + 1);
     HIPCHK(hipMemcpyAsync(off.data(), f->offsets + first_frame, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                          ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+                          ls));
+    HIPCHK(hipStreamSynchronize(ls));
     const uint64_t bytes = off[n] - off[0];
     if (ctx->h_stage_bytes < bytes)
     {
@@ -1262,8 +1302,8 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
         HIPCHK(hipHostMalloc((void **)&ctx->h_stage, bytes, 0));
         ctx->h_stage_bytes = bytes;
     }
-    HIPCHK(hipMemcpyAsync(ctx->h_stage, f->data + off[0], bytes, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->h_stage, f->data + off[0], bytes, hipMemcpyDeviceToHost, ls));
+    HIPCHK(hipStreamSynchronize(ls));
     for (uint32_t i = 0; i < n; ++i)
     {
         const uint64_t len = off[i + 1] - off[i];

@@ -26,6 +26,7 @@ enum
     OPT_LITERAL,
     OPT_SINGLEFOLD,
     OPT_PCAP,
+    OPT_TX,
 };
 
 static const struct option af_xdp_opts[] = {
@@ -43,6 +44,7 @@ static const struct option af_xdp_opts[] = {
     {"literal", no_argument, NULL, OPT_LITERAL},
     {"singlefold", no_argument, NULL, OPT_SINGLEFOLD},
     {"pcap", required_argument, NULL, OPT_PCAP},
+    {"tx", required_argument, NULL, OPT_TX},
     {NULL, 0, NULL, 0},
 };
 
@@ -104,6 +106,9 @@ void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *c, int argc, char **argv)
             break;
         case OPT_PCAP:
             c->pcap = optarg;
+            break;
+        case OPT_TX:
+            c->tx = optarg;
             break;
         default:
             break;

@@ -31,6 +31,7 @@ typedef struct cmd_line_af_xdp
     int literal_payload; /* --literal: reference's as-compiled payload loop (quirk B1) */
     int single_fold;     /* --singlefold: one-fold IPv4 checksum (quirk B6) */
     const char *pcap;    /* --pcap FILE: write built frames to a pcap file */
+    const char *tx;      /* --tx xsk: AF_XDP sockets; otherwise the in-memory TX ring (xsk_ring.h) */
 } cmd_line_af_xdp_t;
 
 void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *cmd_af_xdp, int argc, char **argv);

@@ -9,13 +9,16 @@
  * The JSON config (-c, default /etc/pcktbatch/conf.json) is read first and the
  * -z overrides are applied to its first sequence afterwards, as main.c:90-103
  * does with PB-Common's parse_config() / parse_cli() (host/config_json.c).
- * Frames go to the TX hook: a pcap file with --pcap, otherwise counted.
+ * Frames go through a TX ring: an AF_XDP socket per thread with --tx xsk,
+ * otherwise the in-memory ring of host/xsk_ring.c, whose consumer writes a pcap
+ * file with --pcap (or only counts).
  */
 #include <getopt.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "cmd_line.h"
 #include "config_json.h"
@@ -76,6 +79,7 @@ static const struct option common_opts[] = {
     {"gpu", required_argument, NULL, O_SECOND_PASS}, {"gpubatch", required_argument, NULL, O_SECOND_PASS},
     {"seed", required_argument, NULL, O_SECOND_PASS}, {"literal", no_argument, NULL, O_SECOND_PASS},
     {"singlefold", no_argument, NULL, O_SECOND_PASS}, {"pcap", required_argument, NULL, O_SECOND_PASS},
+    {"tx", required_argument, NULL, O_SECOND_PASS},
     {NULL, 0, NULL, 0},
 };
 
@@ -172,7 +176,7 @@ static void print_cmd_help(void)
                     "-h --help => Print out help menu and exit program.\n"
                     "-z --cli => Enables the first sequence/packet override (README.md first-sequence options).\n\n"
                     "AF_XDP: --queue --nowakeup --sharedumem --batchsize --skb --zerocopy --copy\n"
-                    "GPU: --gpus N --gpu I --gpubatch K --seed S --literal --singlefold --pcap FILE\n");
+                    "GPU: --gpus N --gpu I --gpubatch K --seed S --literal --singlefold --pcap FILE --tx xsk\n");
 }
 
 int main(int argc, char **argv)
@@ -236,10 +240,10 @@ int main(int argc, char **argv)
         fprintf(stdout, "AF_XDP: queue_set=%u queue=%d nowakeup=%u sharedumem=%u batchsize=%u skb=%u zerocopy=%u copy=%u\n",
                 cmd_af_xdp.queue_set, cmd_af_xdp.queue, cmd_af_xdp.no_wake_up, cmd_af_xdp.shared_umem,
                 cmd_af_xdp.batch_size, cmd_af_xdp.skb_mode, cmd_af_xdp.zero_copy, cmd_af_xdp.copy);
-        fprintf(stdout, "GPU: gpus=%d gpu=%d gpubatch=%llu seed=%llu literal=%d singlefold=%d pcap=%s\n",
+        fprintf(stdout, "GPU: gpus=%d gpu=%d gpubatch=%llu seed=%llu literal=%d singlefold=%d pcap=%s tx=%s\n",
                 cmd_af_xdp.gpus, cmd_af_xdp.gpu_first, (unsigned long long)cmd_af_xdp.gpu_batch,
                 (unsigned long long)cmd_af_xdp.seed_base, cmd_af_xdp.literal_payload, cmd_af_xdp.single_fold,
-                cmd_af_xdp.pcap ? cmd_af_xdp.pcap : "(none)");
+                cmd_af_xdp.pcap ? cmd_af_xdp.pcap : "(none)", cmd_af_xdp.tx ? cmd_af_xdp.tx : "ring");
         for (int i = 0; i < seq_cnt; ++i)
             fprintf(stdout, "Sequence #%d: %s -> %s proto %s, %u payload(s)\n", i + 1,
                     cfg->seq[i].ip.src_ip ? cfg->seq[i].ip.src_ip
@@ -261,11 +265,22 @@ int main(int argc, char **argv)
     }
     signal(SIGINT, sign_hdl);
     signal(SIGTERM, sign_hdl);
-    for (int i = 0; i < seq_cnt; ++i)
+    for (int i = 0; i < seq_cnt && !pb_stop_requested(); ++i)
+    {
         seq_send(cfg->interface, cfg->seq[i], (uint16_t)seq_cnt, cmd_af_xdp);
-    shutdown_prog(cfg, 0);
+        /* main.c:113 (a second between sequences; PB_SEQ_GAP_MS shortens it for tests) */
+        const char *gap = getenv("PB_SEQ_GAP_MS");
+        const long ms = gap ? atol(gap) : 1000;
+        for (long t = 0; t < ms && !pb_stop_requested(); t += 10)
+        {
+            struct timespec ts = {0, (ms - t < 10 ? ms - t : 10) * 1000000L};
+            nanosleep(&ts, NULL);
+        }
+    }
+    /* shutdown_prog (sequence.c:779-824) without its exit(): the pcap file is closed
+     * and the memory freed before returning */
+    const int err = pb_shutdown_stats(cfg);
     pb_pcap_close(pcap);
-    const int err = pb_last_error();
     free(cfg);
     free(argv_cli);
     pb_config_free();

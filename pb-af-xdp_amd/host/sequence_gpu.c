@@ -1,17 +1,22 @@
 /*
  * sequence_gpu.c — seq_send() / shutdown_prog() over libpbgpu (see .h).
  *
- * Per sequence: one worker pthread per GPU.  GPU g of n builds iterations
- * [k, k + batch) with k = (step * n + g) * batch, lands the frames in its own
- * UMEM (NUM_FRAMES x FRAME_SIZE, page-aligned and HIP-registered like the
- * reference's posix_memalign'd UMEM, af_xdp.c:374-389) and calls the TX hook
- * per frame.  Counters follow sequence.c:633-653; the stop conditions
- * (max_pckts, max_bytes, time, sequence.c:662-684) and pacing (pps, bps,
- * delay, sequence.c:389-431, 655-659) are applied per launch.
+ * One worker pthread per TX thread of a sequence (the reference's thread_hdl,
+ * sequence.c:33-700, with the per-packet build moved to the GPU):
+ *   setup      MACs (sequence.c:111-136), pbgpu_load_sequence (the template,
+ *              sequence.c:138-374), a page-aligned UMEM registered with HIP
+ *              (af_xdp.c:374-389), the TX queue (AF_XDP socket or loopback);
+ *   loop       claim a batch of iterations (the max_pckts quota, exact across
+ *              threads), build it on the GPU while the previous batch is
+ *              landed in UMEM slots and submitted on the TX ring
+ *              (send_packet/complete_tx, af_xdp.c:25-53, 178-241), count
+ *              (sequence.c:633-653), pace (pps / bps / delay, sequence.c:389-431,
+ *              655-659) and check the stop conditions (sequence.c:662-684).
  */
 #define _GNU_SOURCE
 #include "sequence_gpu.h"
 #include "mac.h"
+#include "xsk_ring.h"
 
 #include <errno.h>
 #include <pthread.h>
@@ -21,14 +26,18 @@
 #include <time.h>
 #include <unistd.h>
 
-#define PB_MAX_WORKERS 64
+#define PB_MAX_WORKERS 1024
+#define PB_BATCH_BYTES_MAX (256ull << 20) /* device bytes per frame buffer (two per worker) */
 
 static uint64_t total_pckts[PB_MAX_SEQUENCES];
 static uint64_t total_bytes[PB_MAX_SEQUENCES];
+static uint64_t claimed_frames[PB_MAX_SEQUENCES]; /* max_pckts quota handed to workers */
+static uint64_t tx_descs[PB_MAX_SEQUENCES], tx_comps[PB_MAX_SEQUENCES], tx_wakeups[PB_MAX_SEQUENCES];
 static time_t start_time[PB_MAX_SEQUENCES];
 static time_t end_time[PB_MAX_SEQUENCES];
 static uint16_t seq_cnt;
-static pthread_t workers[PB_MAX_SEQUENCES * 8];
+static pthread_t workers[PB_MAX_WORKERS];
+static uint8_t joined[PB_MAX_WORKERS];
 static int worker_cnt;
 static int last_error;
 static int verbose;
@@ -41,16 +50,10 @@ void pb_request_stop(void)
     stop_requested = 1;
 }
 
-typedef struct worker_arg
+int pb_stop_requested(void)
 {
-    pb_sequence_t seq;
-    const char *device; /* the interface seq_send() was given (MAC discovery) */
-    uint16_t seq_idx;
-    int gpu;
-    int shard;
-    int n_shards;
-    struct cmd_line_af_xdp cmd;
-} worker_arg_t;
+    return stop_requested;
+}
 
 void pb_set_tx_hook(pb_tx_fn fn, void *ctx)
 {
@@ -79,6 +82,95 @@ int pb_sequence_totals(uint16_t seq, uint64_t *pckts, uint64_t *bytes)
     return PBGPU_OK;
 }
 
+int pb_sequence_tx_stats(uint16_t seq, uint64_t *descs, uint64_t *completions, uint64_t *wakeups)
+{
+    if (seq >= PB_MAX_SEQUENCES)
+        return PBGPU_EINVAL;
+    if (descs)
+        *descs = __atomic_load_n(&tx_descs[seq], __ATOMIC_RELAXED);
+    if (completions)
+        *completions = __atomic_load_n(&tx_comps[seq], __ATOMIC_RELAXED);
+    if (wakeups)
+        *wakeups = __atomic_load_n(&tx_wakeups[seq], __ATOMIC_RELAXED);
+    return PBGPU_OK;
+}
+
+/* ---------------- the builder: libpbgpu ---------------- */
+
+static int gb_open(int gpu, void **h)
+{
+    pbgpu_ctx *c = NULL;
+    const int rc = pbgpu_open(gpu, &c);
+    if (rc == 0)
+        (void)pbgpu_set_timing(c, PBGPU_TIMING_SPAN); /* a sender never reads per-launch timings */
+    *h = c;
+    return rc;
+}
+static int gb_load(void *h, uint16_t i, const pb_sequence_t *s, const uint8_t *sm, const uint8_t *dm,
+                   const pb_rules_t *r, uint64_t seed)
+{
+    return pbgpu_load_sequence((pbgpu_ctx *)h, i, s, sm, dm, r, seed);
+}
+static int gb_alloc(void *h, uint16_t i, uint64_t n_iter, void **frames)
+{
+    uint64_t mf = 0, mb = 0;
+    int rc = pbgpu_build_size((pbgpu_ctx *)h, i, n_iter, &mf, &mb);
+    if (rc == 0)
+        rc = pbgpu_frames_alloc((pbgpu_ctx *)h, mf, mb, (pbgpu_frames **)frames);
+    return rc;
+}
+static int gb_build(void *h, uint16_t i, uint64_t k, uint64_t n, void *frames)
+{
+    return pbgpu_build((pbgpu_ctx *)h, i, k, n, (pbgpu_frames *)frames);
+}
+static uint64_t gb_n_frames(void *frames)
+{
+    return ((pbgpu_frames *)frames)->n_frames;
+}
+static int gb_land(void *h, void *frames, uint8_t *umem, uint32_t stride, uint32_t slot, uint64_t first, uint32_t n,
+                   uint16_t *lens)
+{
+    return pbgpu_copy_to_umem((pbgpu_ctx *)h, (pbgpu_frames *)frames, umem, stride, slot, first, n, lens);
+}
+static int gb_reg(void *h, void *p, size_t n)
+{
+    return pbgpu_host_register((pbgpu_ctx *)h, p, n);
+}
+static int gb_unreg(void *h, void *p)
+{
+    return pbgpu_host_unregister((pbgpu_ctx *)h, p);
+}
+static void gb_free(void *h, void *frames)
+{
+    pbgpu_frames_free((pbgpu_ctx *)h, (pbgpu_frames *)frames);
+}
+static void gb_close(void *h)
+{
+    pbgpu_close((pbgpu_ctx *)h);
+}
+
+static const pb_builder_t gpu_builder = {gb_open, gb_load, gb_alloc, gb_build, gb_n_frames, gb_land,
+                                         gb_reg,  gb_unreg, gb_free, gb_close};
+static const pb_builder_t *builder = &gpu_builder;
+
+void pb_set_builder(const pb_builder_t *b)
+{
+    builder = b ? b : &gpu_builder;
+}
+
+/* ---------------- worker ---------------- */
+
+typedef struct worker_arg
+{
+    pb_sequence_t seq;
+    const char *device; /* the interface seq_send() was given (MAC discovery, AF_XDP socket) */
+    uint16_t seq_idx;
+    int gpu;
+    int shard;   /* TX thread index = queue id (af_xdp.c:443) */
+    int n_shards;
+    struct cmd_line_af_xdp cmd;
+} worker_arg_t;
+
 static double now_s(void)
 {
     struct timespec ts;
@@ -86,25 +178,82 @@ static double now_s(void)
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
+/* sleep until monotonic time t, in slices that notice a stop request */
+static void sleep_until(double t)
+{
+    for (;;)
+    {
+        const double d = t - now_s();
+        if (d <= 0 || stop_requested)
+            return;
+        const double s = d < 0.01 ? d : 0.01;
+        struct timespec ts = {(time_t)s, (long)((s - (double)(time_t)s) * 1e9)};
+        nanosleep(&ts, NULL);
+    }
+}
+
+/* Claim up to `want` frames of the max_pckts quota (whole iterations of fpi
+ * frames): returns the iterations granted, 0 when the quota is spent.  Claims
+ * are exact across threads and GPUs: the sequence sends max_pckts frames
+ * (rounded up to a whole iteration), where the reference's threads overshoot
+ * by up to one iteration each (sequence.c:662-666). */
+static uint64_t claim_iters(uint16_t idx, uint64_t max_pckts, uint64_t want_iters, uint32_t fpi)
+{
+    if (max_pckts == 0)
+        return want_iters;
+    uint64_t cur = __atomic_load_n(&claimed_frames[idx], __ATOMIC_RELAXED);
+    for (;;)
+    {
+        if (cur >= max_pckts)
+            return 0;
+        uint64_t iters = (max_pckts - cur + fpi - 1) / fpi;
+        if (iters > want_iters)
+            iters = want_iters;
+        if (__atomic_compare_exchange_n(&claimed_frames[idx], &cur, cur + iters * fpi, 0, __ATOMIC_RELAXED,
+                                        __ATOMIC_RELAXED))
+            return iters;
+    }
+}
+
+typedef struct sink_arg
+{
+    int shard;
+    int seq_num;
+} sink_arg_t;
+
+static void tx_sink(void *ctx, const uint8_t *frame, uint32_t len, uint64_t addr)
+{
+    (void)addr;
+    const sink_arg_t *a = (const sink_arg_t *)ctx;
+    if (tx_hook && tx_hook(tx_ctx, a->shard, frame, (uint16_t)len) != 0)
+        fprintf(stderr, "[%d][%d] ERROR - Could not send packet (%d) :: %s.\n", a->seq_num, 1, a->shard,
+                strerror(errno));
+}
+
 static void *gpu_worker(void *p)
 {
     worker_arg_t *w = (worker_arg_t *)p;
     const pb_sequence_t *seq = &w->seq;
     const int seq_num = w->seq_idx + 1;
-    pbgpu_ctx *ctx = NULL;
-    pbgpu_frames *fr = NULL;
+    const pb_builder_t *B = builder;
+    void *ctx = NULL;
+    void *fr[2] = {NULL, NULL};
     uint8_t *umem = NULL;
+    int registered = 0;
+    pb_xsk_t xsk;
+    memset(&xsk, 0, sizeof xsk);
+    xsk.fd = -1;
+    sink_arg_t sink = {w->shard, seq_num};
+    const size_t umem_bytes = (size_t)PB_NUM_FRAMES * PB_FRAME_SIZE;
     uint16_t lens[PB_NUM_FRAMES];
     int rc;
 
-    if ((rc = pbgpu_open(w->gpu, &ctx)) != 0)
+    if ((rc = B->open(w->gpu, &ctx)) != 0)
     {
         fprintf(stderr, "[%d] Error opening GPU %d :: %s.\n", seq_num, w->gpu, pbgpu_strerror(rc));
         last_error = rc;
         goto out;
     }
-    /* a continuous sender never reads per-launch timings: no event pair per batch */
-    (void)pbgpu_set_timing(ctx, PBGPU_TIMING_SPAN);
     pb_rules_t rules = {w->cmd.literal_payload ? PB_PAYLOAD_LITERAL : PB_PAYLOAD_STREAM,
                         w->cmd.single_fold ? PB_FOLD_SINGLE : PB_FOLD_FULL};
     /* MACs: a zero source MAC is the device's, a zero destination MAC the default
@@ -133,120 +282,237 @@ static void *gpu_worker(void *p)
         printf("[%d] Destination MAC address => %hhx:%hhx:%hhx:%hhx:%hhx:%hhx.\n", seq_num, dmac[0], dmac[1], dmac[2],
                dmac[3], dmac[4], dmac[5]);
     }
-    if ((rc = pbgpu_load_sequence(ctx, w->seq_idx, seq, smac, dmac, &rules, w->cmd.seed_base)) != 0)
+    if ((rc = B->load(ctx, w->seq_idx, seq, smac, dmac, &rules, w->cmd.seed_base)) != 0)
     {
         fprintf(stderr, "[%d] Error loading sequence on GPU %d :: %s.\n", seq_num, w->gpu, pbgpu_strerror(rc));
         last_error = rc;
         goto out;
     }
-    const uint64_t batch = w->cmd.gpu_batch ? w->cmd.gpu_batch : (1u << 20);
-    uint64_t mf = 0, mb = 0;
-    if ((rc = pbgpu_build_size(ctx, w->seq_idx, batch, &mf, &mb)) != 0 ||
-        (rc = pbgpu_frames_alloc(ctx, mf, mb, &fr)) != 0)
+    const uint32_t fpi = seq->pl_cnt < 1 ? 1u : seq->pl_cnt;
+    uint32_t max_flen = 42 + 12; /* headers */
+    for (uint16_t i = 0; i < seq->pl_cnt; ++i)
+        max_flen += seq->pls[i].max_len > 0 ? seq->pls[i].max_len : 1024; /* static lengths are bounded by the parser */
+    uint64_t batch = w->cmd.gpu_batch ? w->cmd.gpu_batch : (1u << 20);
+    while (batch > 1 && batch * fpi * max_flen > PB_BATCH_BYTES_MAX)
+        batch >>= 1;
+    /* launch-level pacing: one launch covers at most ~1/10 s of the configured rate
+     * (pps, bps and pps are global over the sequence's threads; delay is per thread
+     * and per packet, sequence.c:655-659) */
+    if (seq->pps > 0)
+    {
+        const uint64_t cap = seq->pps / (10ull * (uint64_t)w->n_shards * fpi);
+        batch = batch < (cap ? cap : 1) ? batch : (cap ? cap : 1);
+    }
+    if (seq->bps > 0)
+    {
+        const uint64_t cap = seq->bps / (10ull * (uint64_t)w->n_shards * fpi * max_flen);
+        batch = batch < (cap ? cap : 1) ? batch : (cap ? cap : 1);
+    }
+    if (seq->delay > 0)
+    {
+        const uint64_t cap = 100000ull / ((uint64_t)seq->delay * fpi);
+        batch = batch < (cap ? cap : 1) ? batch : (cap ? cap : 1);
+    }
+    if ((rc = B->alloc(ctx, w->seq_idx, batch, &fr[0])) != 0 || (rc = B->alloc(ctx, w->seq_idx, batch, &fr[1])) != 0)
     {
         last_error = rc;
         goto out;
     }
-    if (posix_memalign((void **)&umem, (size_t)sysconf(_SC_PAGESIZE), (size_t)PB_NUM_FRAMES * PB_FRAME_SIZE) != 0)
+    if (posix_memalign((void **)&umem, (size_t)sysconf(_SC_PAGESIZE), umem_bytes) != 0)
     {
+        umem = NULL;
         last_error = PBGPU_ENOMEM;
         goto out;
     }
-    memset(umem, 0, (size_t)PB_NUM_FRAMES * PB_FRAME_SIZE);
-    pbgpu_host_register(ctx, umem, (size_t)PB_NUM_FRAMES * PB_FRAME_SIZE);
+    memset(umem, 0, umem_bytes);
+    registered = B->host_register(ctx, umem, umem_bytes) == 0;
+
+    /* the TX queue: an AF_XDP socket on queue `shard` (or --queue, af_xdp.c:443),
+     * or the in-memory loopback whose consumer hands frames to the TX hook */
+    if (w->cmd.tx && strcmp(w->cmd.tx, "xsk") == 0)
+    {
+        uint16_t bf = w->cmd.no_wake_up ? 0 : XDP_USE_NEED_WAKEUP;
+        if (w->cmd.zero_copy)
+            bf |= XDP_ZEROCOPY;
+        else if (w->cmd.copy)
+            bf |= XDP_COPY;
+        const uint32_t q = w->cmd.queue_set ? (uint32_t)w->cmd.queue : (uint32_t)w->shard;
+        if ((rc = pb_xsk_open(&xsk, w->device, q, umem, PB_NUM_FRAMES, PB_FRAME_SIZE, bf)) != 0)
+        {
+            fprintf(stderr, "Could not setup AF_XDP socket at index %d :: %s (%d).\n", w->shard, strerror(-rc), -rc);
+            last_error = rc;
+            goto out;
+        }
+    }
+    else if ((rc = pb_xsk_loopback(&xsk, umem, PB_NUM_FRAMES, PB_FRAME_SIZE)) != 0)
+    {
+        last_error = rc;
+        goto out;
+    }
+    else
+    {
+        xsk.loop_sink = tx_hook ? tx_sink : NULL;
+        xsk.loop_ctx = &sink;
+    }
 
     const double t0 = now_s();
-    const int fpi = seq->pl_cnt < 1 ? 1 : seq->pl_cnt;
-    for (uint64_t step = 0; !stop_requested; ++step)
+    uint64_t my_frames = 0; /* this thread's frames: the delay pacing (per thread) */
+    uint64_t step = 0;
+    int cur = 0;
+    /* batch `step` covers iterations [(step * n_shards + shard) * batch, + n_iter) */
+    uint64_t n_cur = claim_iters(w->seq_idx, seq->max_pckts, batch, fpi);
+    if (n_cur && (rc = B->build(ctx, w->seq_idx, ((uint64_t)w->shard) * batch, n_cur, fr[cur])) != 0)
     {
-        uint64_t n_iter = batch;
-        if (seq->max_pckts > 0) /* launch-level quota of the global counter */
-        {
-            uint64_t done = __atomic_load_n(&total_pckts[w->seq_idx], __ATOMIC_RELAXED);
-            if (done >= seq->max_pckts)
-                break;
-            uint64_t left = (seq->max_pckts - done + fpi - 1) / fpi;
-            left = (left + w->n_shards - 1) / w->n_shards;
-            if (left < n_iter)
-                n_iter = left;
-        }
-        const uint64_t k = (step * (uint64_t)w->n_shards + (uint64_t)w->shard) * batch;
-        if ((rc = pbgpu_build(ctx, w->seq_idx, k, n_iter, fr)) != 0)
+        fprintf(stderr, "[%d] Error building frames on GPU %d :: %s.\n", seq_num, w->gpu, pbgpu_strerror(rc));
+        last_error = rc;
+        goto out;
+    }
+    int done = n_cur == 0 ? 4 : 0; /* 1 max bytes, 2 time, 3 error, 4 quota spent */
+    while (!done && !stop_requested)
+    {
+        /* double buffering: the next batch builds on the GPU while this one lands */
+        const uint64_t n_next = claim_iters(w->seq_idx, seq->max_pckts, batch, fpi);
+        if (n_next &&
+            (rc = B->build(ctx, w->seq_idx, ((step + 1) * (uint64_t)w->n_shards + (uint64_t)w->shard) * batch, n_next,
+                           fr[cur ^ 1])) != 0)
         {
             fprintf(stderr, "[%d] Error building frames on GPU %d :: %s.\n", seq_num, w->gpu, pbgpu_strerror(rc));
             last_error = rc;
             break;
         }
-        uint64_t bytes = 0;
-        for (uint64_t f0 = 0; f0 < fr->n_frames; f0 += PB_NUM_FRAMES)
+        const uint64_t nf = B->n_frames(fr[cur]);
+        uint64_t f0 = 0;
+        while (f0 < nf && !done && !stop_requested)
         {
-            const uint32_t n = (uint32_t)(fr->n_frames - f0 < PB_NUM_FRAMES ? fr->n_frames - f0 : PB_NUM_FRAMES);
-            if ((rc = pbgpu_copy_to_umem(ctx, fr, umem, PB_FRAME_SIZE, 0, f0, n, lens)) != 0)
+            /* land as many frames as free UMEM slots allow, in slot-ring order */
+            while (pb_xsk_free_slots(&xsk) == 0 && !stop_requested)
+                if (pb_xsk_complete(&xsk, PB_NUM_FRAMES) == 0)
+                    sched_yield();
+            if (stop_requested)
+                break;
+            uint32_t n = pb_xsk_free_slots(&xsk);
+            if ((uint64_t)n > nf - f0)
+                n = (uint32_t)(nf - f0);
+            const uint32_t slot = xsk.next_slot;
+            const uint32_t n1 = n < PB_NUM_FRAMES - slot ? n : PB_NUM_FRAMES - slot; /* the slot ring wraps */
+            if ((rc = B->land(ctx, fr[cur], umem, PB_FRAME_SIZE, slot, f0, n1, lens)) != 0 ||
+                (n1 < n && (rc = B->land(ctx, fr[cur], umem, PB_FRAME_SIZE, 0, f0 + n1, n - n1, lens + n1)) != 0))
             {
+                fprintf(stderr, "[%d] Error landing frames from GPU %d :: %s.\n", seq_num, w->gpu, pbgpu_strerror(rc));
                 last_error = rc;
-                goto out;
+                done = 3;
+                break;
             }
+            uint64_t bytes = 0;
             for (uint32_t i = 0; i < n; ++i)
-            {
                 bytes += lens[i];
-                if (tx_hook && tx_hook(tx_ctx, w->shard, umem + (size_t)i * PB_FRAME_SIZE, lens[i]) != 0)
-                    fprintf(stderr, "[%d][%d] ERROR - Could not send packet (%d) :: %s.\n", seq_num, i + 1, w->shard,
-                            strerror(errno));
+            if (seq->max_bytes > 0) /* send until the total reaches max_bytes (sequence.c:668-674) */
+            {
+                uint64_t tot = __atomic_load_n(&total_bytes[w->seq_idx], __ATOMIC_RELAXED);
+                for (;;)
+                {
+                    if (tot >= seq->max_bytes)
+                    {
+                        n = 0, bytes = 0;
+                        break;
+                    }
+                    uint32_t m = 0;
+                    uint64_t b = 0;
+                    while (m < n && tot + b < seq->max_bytes)
+                        b += lens[m++];
+                    if (__atomic_compare_exchange_n(&total_bytes[w->seq_idx], &tot, tot + b, 0, __ATOMIC_RELAXED,
+                                                    __ATOMIC_RELAXED))
+                    {
+                        n = m, bytes = b;
+                        break;
+                    }
+                }
+                if (n == 0)
+                {
+                    done = 1;
+                    break;
+                }
             }
+            else
+                __atomic_add_fetch(&total_bytes[w->seq_idx], bytes, __ATOMIC_RELAXED);
+            if ((rc = pb_xsk_send(&xsk, lens, n)) != 0)
+            {
+                fprintf(stderr, "[%d][%d] ERROR - Could not send packet on AF_XDP socket (%d) :: %s.\n", seq_num, 1,
+                        w->shard, strerror(-rc));
+                last_error = rc;
+                done = 3;
+                break;
+            }
+            __atomic_add_fetch(&total_pckts[w->seq_idx], n, __ATOMIC_RELAXED);
+            my_frames += n;
+            f0 += n;
+
+            /* pacing (sequence.c:389-431, 655-659) at landing-chunk granularity: pps and
+             * bps against the sequence's global totals, delay per thread and packet */
+            double want = 0;
+            if (seq->pps > 0)
+                want = (double)__atomic_load_n(&total_pckts[w->seq_idx], __ATOMIC_RELAXED) / (double)seq->pps;
+            if (seq->bps > 0)
+            {
+                const double wb = (double)__atomic_load_n(&total_bytes[w->seq_idx], __ATOMIC_RELAXED) /
+                                  (double)seq->bps; /* bytes per second (README.md:113, sequence.c:650-652) */
+                want = wb > want ? wb : want;
+            }
+            if (seq->delay > 0)
+            {
+                const double wd = (double)my_frames * (double)seq->delay * 1e-6;
+                want = wd > want ? wd : want;
+            }
+            if (want > 0)
+                sleep_until(t0 + want);
+            if (seq->time > 0 && now_s() - t0 >= (double)seq->time)
+                done = 2;
         }
-        __atomic_add_fetch(&total_pckts[w->seq_idx], fr->n_frames, __ATOMIC_RELAXED);
-        __atomic_add_fetch(&total_bytes[w->seq_idx], bytes, __ATOMIC_RELAXED);
         if (verbose)
-            fprintf(stdout, "[%d] GPU %d built %llu frames (%llu bytes) from iteration %llu.\n", seq_num, w->gpu,
-                    (unsigned long long)fr->n_frames, (unsigned long long)bytes, (unsigned long long)k);
-
-        /* pacing at launch granularity (sequence.c:389-431, 655-659) */
-        const double el = now_s() - t0;
-        double want = 0;
-        const double frames = (double)__atomic_load_n(&total_pckts[w->seq_idx], __ATOMIC_RELAXED) / w->n_shards;
-        if (seq->pps > 0)
-            want = frames / (double)seq->pps;
-        if (seq->bps > 0)
-        {
-            const double b = (double)__atomic_load_n(&total_bytes[w->seq_idx], __ATOMIC_RELAXED) / w->n_shards;
-            const double wb = b / (double)seq->bps;
-            want = wb > want ? wb : want;
-        }
-        if (seq->delay > 0)
-        {
-            const double wd = frames * (double)seq->delay * 1e-6;
-            want = wd > want ? wd : want;
-        }
-        if (want > el)
-            usleep((useconds_t)((want - el) * 1e6));
-
-        if (seq->max_pckts > 0 && __atomic_load_n(&total_pckts[w->seq_idx], __ATOMIC_RELAXED) >= seq->max_pckts)
+            fprintf(stdout, "[%d] Thread %d (GPU %d) sent %llu frames of iteration batch %llu.\n", seq_num, w->shard,
+                    w->gpu, (unsigned long long)f0, (unsigned long long)step);
+        if (seq->max_pckts > 0 && n_next == 0 &&
+            __atomic_load_n(&claimed_frames[w->seq_idx], __ATOMIC_RELAXED) >= seq->max_pckts)
         {
             fprintf(stdout, "[%d] Max packets exceeded for sequence. Stopping...\n", seq_num);
             break;
         }
-        if (seq->max_bytes > 0 && __atomic_load_n(&total_bytes[w->seq_idx], __ATOMIC_RELAXED) >= seq->max_bytes)
+        if (done == 1 && seq->max_bytes > 0)
         {
             fprintf(stdout, "[%d] Max bytes exceeded for sequence. Stopping...\n", seq_num);
             break;
         }
-        if (seq->time > 0 && now_s() - t0 >= (double)seq->time)
+        if (done == 2 || (seq->time > 0 && now_s() - t0 >= (double)seq->time))
         {
             fprintf(stdout, "[%d] Time exceeded for sequence. Stopping...\n", seq_num);
             break;
         }
+        if (done || n_next == 0)
+            break;
+        cur ^= 1;
+        ++step;
     }
+    /* drain: every submitted frame completes before the UMEM goes away */
+    for (int spin = 0; xsk.outstanding_tx && spin < 100000; ++spin)
+        if (pb_xsk_complete(&xsk, PB_NUM_FRAMES) == 0)
+            sched_yield();
 out:
     end_time[w->seq_idx] = time(NULL);
+    __atomic_add_fetch(&tx_descs[w->seq_idx], xsk.completed + xsk.outstanding_tx, __ATOMIC_RELAXED);
+    __atomic_add_fetch(&tx_comps[w->seq_idx], xsk.completed, __ATOMIC_RELAXED);
+    __atomic_add_fetch(&tx_wakeups[w->seq_idx], xsk.wakeups, __ATOMIC_RELAXED);
+    pb_xsk_close(&xsk);
     if (umem)
     {
-        if (ctx)
-            pbgpu_host_unregister(ctx, umem);
+        if (registered)
+            B->host_unregister(ctx, umem);
         free(umem);
     }
-    if (fr)
-        pbgpu_frames_free(ctx, fr);
-    pbgpu_close(ctx);
+    for (int i = 0; i < 2; ++i)
+        if (fr[i])
+            B->free_frames(ctx, fr[i]);
+    if (ctx)
+        B->close(ctx);
     free(w);
     return NULL;
 }
@@ -263,13 +529,17 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
         fprintf(stderr, "Destination IP not set on sequence #%d. Not moving forward with this sequence.\n", seqc);
         return;
     }
+    if (seq_cnt >= PB_MAX_SEQUENCES)
+        return;
     const uint16_t idx = seq_cnt++;
-    int n = cmd.gpus > 0 ? cmd.gpus : 1;
-    if (n > PB_MAX_WORKERS)
-        n = PB_MAX_WORKERS;
+    const int gpus = cmd.gpus > 0 ? cmd.gpus : 1;
+    /* TX threads (sequence.c:741): the sequence's `threads`, else one per GPU */
+    int t_cnt = seq.threads > 0 ? seq.threads : gpus;
+    if (t_cnt > PB_MAX_WORKERS - worker_cnt)
+        t_cnt = PB_MAX_WORKERS - worker_cnt;
     start_time[idx] = time(NULL);
     const int old = worker_cnt;
-    for (int g = 0; g < n; ++g)
+    for (int t = 0; t < t_cnt; ++t)
     {
         worker_arg_t *w = (worker_arg_t *)calloc(1, sizeof *w);
         if (w == NULL)
@@ -277,27 +547,37 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
         w->seq = seq;
         w->device = interface;
         w->seq_idx = idx;
-        w->gpu = cmd.gpu_first + g;
-        w->shard = g;
-        w->n_shards = n;
+        w->gpu = cmd.gpu_first + t % gpus;
+        w->shard = t;
+        w->n_shards = t_cnt;
         w->cmd = cmd;
         if (pthread_create(&workers[worker_cnt], NULL, gpu_worker, w) != 0)
         {
             free(w);
             break;
         }
+        joined[worker_cnt] = 0;
         ++worker_cnt;
     }
     if (seq.block || seq_cnt >= seqc - 1) /* sequence.c:765, including its off-by-one (B10) */
         for (int i = old; i < worker_cnt; ++i)
+        {
             pthread_join(workers[i], NULL);
+            joined[i] = 1;
+        }
 }
 
-void shutdown_prog(pb_config_t *cfg, int exit_prog)
+int pb_shutdown_stats(pb_config_t *cfg)
 {
+    /* the reference cancels its threads (sequence.c:781-784); these stop after their
+     * current batch, and each is joined exactly once */
+    pb_request_stop();
     for (int i = 0; i < worker_cnt; ++i)
-        pthread_join(workers[i], NULL);
-    worker_cnt = 0;
+        if (!joined[i])
+        {
+            pthread_join(workers[i], NULL);
+            joined[i] = 1;
+        }
     fprintf(stdout, "Completed %d sequences!\n", seq_cnt);
     for (int i = 0; i < seq_cnt && cfg; ++i)
     {
@@ -315,8 +595,35 @@ void shutdown_prog(pb_config_t *cfg, int exit_prog)
                 i + 1, (unsigned long long)p, (unsigned long long)b, (unsigned long long)(p / secs),
                 (unsigned long long)(b / secs), (long)secs);
     }
-    if (exit_prog)
-        exit(last_error ? EXIT_FAILURE : EXIT_SUCCESS);
+    fflush(stdout);
+    return last_error;
+}
+
+void shutdown_prog(pb_config_t *cfg)
+{
+    const int err = pb_shutdown_stats(cfg);
+    free(cfg);
+    exit(err ? EXIT_FAILURE : EXIT_SUCCESS);
+}
+
+void pb_reset(void)
+{
+    pb_request_stop();
+    for (int i = 0; i < worker_cnt; ++i)
+        if (!joined[i])
+            pthread_join(workers[i], NULL);
+    worker_cnt = 0;
+    seq_cnt = 0;
+    last_error = 0;
+    memset(total_pckts, 0, sizeof total_pckts);
+    memset(total_bytes, 0, sizeof total_bytes);
+    memset(claimed_frames, 0, sizeof claimed_frames);
+    memset(tx_descs, 0, sizeof tx_descs);
+    memset(tx_comps, 0, sizeof tx_comps);
+    memset(tx_wakeups, 0, sizeof tx_wakeups);
+    memset(start_time, 0, sizeof start_time);
+    memset(end_time, 0, sizeof end_time);
+    stop_requested = 0;
 }
 
 /* ---- pcap TX hook ---- */

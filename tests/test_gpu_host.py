@@ -78,11 +78,53 @@ def test_json_config_sequences_equal_oracle(tmp_path):
     path = tmp_path / "conf.json"
     path.write_text(json.dumps({"interface": "pbnodev0", "sequences": seqs}))
     pcap = tmp_path / "mix.pcap"
+    import time
+
+    t0 = time.perf_counter()
     r = subprocess.run([BIN, "-c", str(path), "--gpubatch", "1024", "--seed", "99", "--pcap", str(pcap)],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Completed 3 sequences!" in r.stdout
+    assert time.perf_counter() - t0 > 2.5  # main.c:113: a second after each sequence
     want = []
     for i, c in enumerate(seqs):
         want += ob.frames(Sequence.from_config(c), i, 0, c["maxpckts"], 99)
     assert read_pcap(pcap) == want
+
+
+def test_cli_two_threads_send_distinct_iterations(tmp_path):
+    """--threads 2 on one GPU (sequence.c:741: one TX thread per queue, here two
+    pbgpu contexts on one GPU): the max_pckts quota is split exactly and every
+    frame sent is a distinct iteration's frame of the seed stream."""
+    pcap = tmp_path / "t2.pcap"
+    seed = 4242
+    cmd = [BIN, "-z", "--interface", "pbnodev0", "--smac", pc.SMAC, "--dmac", pc.DMAC, "--dip", pc.DIP,
+           "--sip", "10.20.0.0/16", "--protocol", "udp", "--udport", "27015", "--pmin", "22", "--pmax", "22",
+           "--maxpckts", "6000", "--delay", "0", "--threads", "2", "--gpubatch", "1000", "--seed", str(seed),
+           "--pcap", str(pcap)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    got = read_pcap(pcap)
+    assert len(got) == 6000 and len(set(got)) == 6000
+    # thread t builds iterations (step * 2 + t) * 1000 + j: all within [0, 12000)
+    universe = set(ob.frames(Sequence.from_config(pc.c2_udp_64()), 0, 0, 12000, seed))
+    assert set(got) <= universe
+
+
+def test_cli_null_tx_end_to_end(tmp_path):
+    """Build -> land in UMEM slots -> TX descriptors on the in-memory ring, no pcap:
+    the end-to-end rate of the host pipeline (DESIGN.md §6 records the numbers)."""
+    import time
+
+    n = 1 << 22
+    cmd = [BIN, "-z", "--interface", "pbnodev0", "--smac", pc.SMAC, "--dmac", pc.DMAC, "--dip", pc.DIP,
+           "--sip", "10.20.0.0/16", "--protocol", "udp", "--udport", "27015", "--pmin", "22", "--pmax", "22",
+           "--maxpckts", str(n), "--delay", "0", "--track", "1", "--gpubatch", str(1 << 18)]
+    env = dict(os.environ, PB_SEQ_GAP_MS="0")
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    dt = time.perf_counter() - t0
+    assert r.returncode == 0, r.stderr
+    assert f"total of {n} packets and {64 * n} bytes" in r.stdout
+    print(f"end-to-end (null TX ring, 64-B frames): {n / dt / 1e6:.1f} Mpps incl. process start")
+    assert n / dt > 20e6

@@ -1,0 +1,336 @@
+"""The host TX path on the CPU (no GPU): the libbpf-free AF_XDP ring protocol
+(host/xsk_ring.c: send_packet / complete_tx, af_xdp.c:25-53, 178-241) on the
+in-memory loopback, and the seq_send worker loop (host/sequence_gpu.c) with a
+CPU stand-in for the GPU builder (tests/host_stub.c): the max_pckts quota across
+threads, max_bytes, time, pps / bps / delay pacing (sequence.c:389-431,
+655-684), the per-sequence thread fan-out (sequence.c:741), the stop request
+and the end-of-run lines (sequence.c:779-815)."""
+import ctypes as C
+import os
+import subprocess
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import pb_configs as pc
+from cmdline_binding import OurCmd
+from pbgpu import Sequence, SequenceT
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "pb-af-xdp_amd", "lib")
+BUILD = os.path.join(ROOT, "tests", "_build")
+STUB = os.path.join(BUILD, "libpbhost_stub.so")
+
+
+@pytest.fixture(scope="module")
+def libs():
+    os.makedirs(BUILD, exist_ok=True)
+    subprocess.run(["gcc", "-O2", "-Wall", "-shared", "-fPIC", "-pthread", "-o", STUB,
+                    os.path.join(ROOT, "tests", "host_stub.c"), "-L" + LIBDIR, "-lpbhost",
+                    "-Wl,-rpath," + LIBDIR], check=True)
+    host = C.CDLL(os.path.join(LIBDIR, "libpbhost.so"))
+    stub = C.CDLL(STUB)
+    host.seq_send.argtypes = [C.c_char_p, SequenceT, C.c_uint16, OurCmd]
+    host.seq_send.restype = None
+    host.pb_shutdown_stats.argtypes = [C.c_void_p]
+    host.pb_sequence_totals.argtypes = [C.c_uint16, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    host.pb_sequence_tx_stats.argtypes = [C.c_uint16] + [C.POINTER(C.c_uint64)] * 3
+    host.cmd_line_af_xdp_defaults.argtypes = [C.POINTER(OurCmd)]
+    stub.ring_stress.argtypes = [C.c_uint32, C.c_uint64, C.POINTER(C.c_uint64)]
+    stub.stub_recorded.restype = C.c_uint64
+    stub.stub_recorded.argtypes = [C.c_void_p] * 4 + [C.c_uint64]
+    stub.stub_record.argtypes = [C.c_uint64]
+    yield host, stub
+    stub.stub_uninstall()
+    host.pb_set_tx_hook(None, None)
+
+
+# ---------------------------------------------------------------- ring protocol
+
+
+class XdpDesc(C.Structure):
+    _fields_ = [("addr", C.c_uint64), ("len", C.c_uint32), ("options", C.c_uint32)]
+
+
+class Ring(C.Structure):
+    _fields_ = [("cached_prod", C.c_uint32), ("cached_cons", C.c_uint32), ("mask", C.c_uint32), ("size", C.c_uint32),
+                ("producer", C.POINTER(C.c_uint32)), ("consumer", C.POINTER(C.c_uint32)),
+                ("flags", C.POINTER(C.c_uint32)), ("ring", C.c_void_p)]
+
+
+class Xsk(C.Structure):
+    _fields_ = [("fd", C.c_int), ("umem", C.c_void_p), ("n_frames", C.c_uint32), ("frame_size", C.c_uint32),
+                ("tx", Ring), ("cq", Ring), ("fq", Ring), ("next_slot", C.c_uint32), ("outstanding_tx", C.c_uint32),
+                ("need_wakeup", C.c_uint32), ("wakeups", C.c_uint64), ("completed", C.c_uint64),
+                ("maps", C.c_void_p * 3), ("map_len", C.c_size_t * 3), ("loop_mem", C.c_void_p),
+                ("loop_auto", C.c_int), ("loop_sink", C.c_void_p), ("loop_ctx", C.c_void_p)]
+
+
+def _loopback(host, n, fs=4096):
+    umem = np.zeros(n * fs + 4096, dtype=np.uint8)
+    base = (umem.ctypes.data + 4095) & ~4095
+    x = Xsk()
+    assert host.pb_xsk_loopback(C.byref(x), C.c_void_p(base), n, fs) == 0
+    return x, umem
+
+
+def test_ring_reserve_submit_consume_complete(libs):
+    host, _ = libs
+    host.pb_ring_prod_reserve.restype = C.c_uint32
+    host.pb_ring_tx_desc.restype = C.POINTER(XdpDesc)
+    host.pb_xsk_loop_consume.restype = C.c_uint32
+    host.pb_xsk_complete.restype = C.c_uint32
+    host.pb_xsk_free_slots.restype = C.c_uint32
+    x, _keep = _loopback(host, 8)
+    x.loop_auto = 0
+    idx = C.c_uint32()
+    # the TX ring holds exactly `size` entries
+    assert host.pb_ring_prod_reserve(C.byref(x.tx), 5, C.byref(idx)) == 5 and idx.value == 0
+    assert host.pb_ring_prod_reserve(C.byref(x.tx), 4, C.byref(idx)) == 0
+    assert host.pb_ring_prod_reserve(C.byref(x.tx), 3, C.byref(idx)) == 3 and idx.value == 5
+    for i in range(8):
+        d = host.pb_ring_tx_desc(C.byref(x.tx), i).contents
+        d.addr, d.len = i * 4096, 60 + i
+    host.pb_ring_prod_submit(C.byref(x.tx), 8)
+    assert x.tx.producer[0] == 8
+    # the kernel side takes 3, completes them; the producer sees 3 free entries again
+    assert host.pb_xsk_loop_consume(C.byref(x), 3, None, None) == 3
+    assert x.tx.consumer[0] == 3 and x.cq.producer[0] == 3
+    assert host.pb_ring_prod_reserve(C.byref(x.tx), 3, C.byref(idx)) == 3 and idx.value == 8
+    # indices wrap: entry 8 is slot 0 of the ring
+    d = host.pb_ring_tx_desc(C.byref(x.tx), 8).contents
+    assert C.addressof(d) == x.tx.ring
+    host.pb_xsk_close(C.byref(x))
+
+
+def test_send_fills_descriptors_and_reaps_completions(libs):
+    host, _ = libs
+    host.pb_xsk_free_slots.restype = C.c_uint32
+    x, _keep = _loopback(host, 16)
+    lens = (C.c_uint16 * 16)(*range(100, 116))
+    # loopback with the kernel side run at every wakeup: each send completes at once
+    for rnd in range(5):
+        assert host.pb_xsk_send(C.byref(x), lens, 11) == 0
+        assert x.outstanding_tx == 0 and x.completed == 11 * (rnd + 1)
+        assert x.next_slot == (11 * (rnd + 1)) % 16
+    assert x.wakeups == 5
+    # without a consumer the UMEM slots run out: the sender is refused, not overwritten
+    x.loop_auto = 0
+    assert host.pb_xsk_send(C.byref(x), lens, 16) == 0
+    assert host.pb_xsk_free_slots(C.byref(x)) == 0
+    assert host.pb_xsk_send(C.byref(x), lens, 1) == -28  # -ENOSPC
+    host.pb_xsk_close(C.byref(x))
+
+
+@pytest.mark.parametrize("n_frames,total", [(8, 5000), (64, 40000), (4096, 200000)])
+def test_ring_protocol_with_kernel_on_another_thread(libs, n_frames, total):
+    """Producer and consumer on different threads: every frame arrives once, in
+    order, with its descriptor's length; every descriptor completes."""
+    _, stub = libs
+    w = C.c_uint64()
+    assert stub.ring_stress(n_frames, total, C.byref(w)) == 0
+    assert w.value > 0
+
+
+def test_af_xdp_socket_setup_fails_cleanly_without_privilege(libs):
+    host, _ = libs
+    x = Xsk()
+    umem = np.zeros(4096 * 4096 + 4096, dtype=np.uint8)
+    base = (umem.ctypes.data + 4095) & ~4095
+    rc = host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 4096, 8)
+    # a negative errno (no AF_XDP / CAP_NET_RAW in this container), or a bound socket
+    assert rc <= 0
+    if rc == 0:
+        host.pb_xsk_close(C.byref(x))
+    assert host.pb_xsk_open(C.byref(x), b"pbnodev0", 0, C.c_void_p(base), 4096, 4096, 8) == -19  # -ENODEV
+
+
+# ---------------------------------------------------------------- worker loop
+
+
+def _cmd(host, **kw):
+    c = OurCmd()
+    host.cmd_line_af_xdp_defaults(C.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def _seq(cfg):
+    s = Sequence.from_config(cfg)
+    return s
+
+
+def _run(libs, cfg, seqc=1, cap=1 << 20, **cmdkw):
+    host, stub = libs
+    host.pb_reset()
+    stub.stub_install()
+    assert stub.stub_record(cap) == 0
+    s = _seq(cfg)
+    t0 = time.perf_counter()
+    host.seq_send(b"lo", s.c, seqc, _cmd(host, **cmdkw))
+    err = host.pb_shutdown_stats(None)
+    dt = time.perf_counter() - t0
+    p, b = C.c_uint64(), C.c_uint64()
+    host.pb_sequence_totals(0, C.byref(p), C.byref(b))
+    n = min(cap, 1 << 22)
+    k = np.zeros(n, dtype=np.uint64)
+    i, ln, th = (np.zeros(n, dtype=np.uint16) for _ in range(3))
+    seen = stub.stub_recorded(k.ctypes.data, i.ctypes.data, ln.ctypes.data, th.ctypes.data, n)
+    m = min(seen, n)
+    return {"err": err, "pckts": p.value, "bytes": b.value, "dt": dt, "seen": seen, "k": k[:m], "i": i[:m],
+            "len": ln[:m], "thread": th[:m], "seq": s}
+
+
+def _cfg(min_len=22, max_len=22, **kw):
+    c = pc.c2_udp_64()
+    c["payloads"] = [{"length": {"min": min_len, "max": max_len}}]
+    c.update(kw)
+    return c
+
+
+def test_single_thread_sends_iterations_in_order(libs):
+    r = _run(libs, _cfg(maxpckts=10000, delay=0), gpu_batch=3000)
+    assert r["err"] == 0 and r["pckts"] == 10000 and r["seen"] == 10000
+    assert np.array_equal(r["k"], np.arange(10000, dtype=np.uint64))
+    assert (r["len"] == 64).all() and r["bytes"] == 64 * 10000
+
+
+@pytest.mark.parametrize("threads,gpus", [(2, 2), (3, 1), (8, 2)])
+def test_maxpckts_quota_is_exact_across_threads(libs, threads, gpus):
+    """The max_pckts quota is claimed per batch: the sequence sends exactly
+    max_pckts frames over all threads / GPUs, every one a distinct iteration of
+    the threads' shards (the reference overshoots by up to a batch per thread)."""
+    maxp = 123457
+    r = _run(libs, _cfg(0, 900, maxpckts=maxp, delay=0, threads=threads), gpus=gpus, gpu_batch=5000)
+    assert r["err"] == 0 and r["pckts"] == maxp and r["seen"] == maxp
+    assert len(np.unique(r["k"])) == maxp
+    # thread t sends iterations of its shard: (step * threads + t) * batch + j
+    assert ((r["k"] // 5000) % threads == r["thread"]).all()
+    assert r["bytes"] == int(r["len"].astype(np.int64).sum())
+    # (a thread that starts late may find the quota already claimed: no per-thread share is promised)
+
+
+def test_maxpckts_with_several_payloads_rounds_to_whole_iterations(libs):
+    cfg = _cfg(maxpckts=1001, delay=0)
+    cfg["payloads"] = [{"length": {"min": 10, "max": 10}}, {"length": {"min": 30, "max": 30}},
+                       {"length": {"min": 50, "max": 50}}]
+    r = _run(libs, cfg, gpu_batch=100)
+    assert r["pckts"] == 1002  # 334 whole iterations of 3 frames
+    assert np.array_equal(np.bincount(r["i"].astype(np.int64)), [334, 334, 334])
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_maxbytes_stops_at_the_byte_budget(libs, threads):
+    maxb = 3_000_000
+    r = _run(libs, _cfg(0, 1400, maxbytes=maxb, delay=0, threads=threads), gpu_batch=2000)
+    assert r["err"] == 0
+    # sends until the total reaches max_bytes (sequence.c:668-674): at most one frame over per thread
+    assert maxb <= r["bytes"] < maxb + threads * 1500
+    assert r["bytes"] == int(r["len"].astype(np.int64).sum()) and r["pckts"] == r["seen"]
+
+
+def test_time_limit(libs):
+    r = _run(libs, _cfg(time=1, delay=100), gpu_batch=1000)
+    assert r["err"] == 0 and 0.9 < r["dt"] < 3.0
+    assert 1000 < r["pckts"] <= 12000  # ~10k frames at one per 100 us
+
+
+def test_pps_limit_is_global_over_threads(libs):
+    """pps limits the sequence, not each thread (sequence.c:389-431: cur_pps is shared)."""
+    r = _run(libs, _cfg(maxpckts=3000, pps=4000, delay=0, threads=3), gpu_batch=100000)
+    assert r["pckts"] == 3000
+    assert 0.55 < r["dt"] < 1.6  # 3000 frames at 4000 pps: 0.75 s
+
+
+def test_bps_limit(libs):
+    # 64-B frames, 128000 bytes per second: 2000 frames per second
+    r = _run(libs, _cfg(maxpckts=1500, bps=128000, delay=0), gpu_batch=100000)
+    assert r["pckts"] == 1500
+    assert 0.55 < r["dt"] < 1.6
+
+
+@pytest.mark.parametrize("threads,want_s", [(1, 0.8), (2, 0.4)])
+def test_delay_is_per_thread_and_per_packet(libs, threads, want_s):
+    """delay sleeps after every packet of every thread (sequence.c:655-659)."""
+    r = _run(libs, _cfg(maxpckts=400, delay=2000, threads=threads), gpu_batch=100000)
+    assert r["pckts"] == 400
+    assert want_s * 0.7 < r["dt"] < want_s * 2 + 0.4
+
+
+def test_default_delay_sends_one_frame_per_second_per_thread(libs):
+    """The README default delay (1,000,000 us) means one packet per second per thread."""
+    host, stub = libs
+    host.pb_reset()
+    stub.stub_install()
+    stub.stub_record(100)
+    s = _seq(_cfg(delay=1000000, threads=2, block=0))
+    t0 = time.perf_counter()
+    host.seq_send(b"lo", s.c, 3, _cmd(host))  # not blocking: returns at once
+    assert time.perf_counter() - t0 < 0.5
+    time.sleep(1.5)
+    host.pb_shutdown_stats(None)  # stops and joins the threads
+    dt = time.perf_counter() - t0
+    p = C.c_uint64()
+    host.pb_sequence_totals(0, C.byref(p), None)
+    assert 1.4 < dt < 3.0
+    assert 2 <= p.value <= 6  # t = 0 and t = 1 s on each of 2 threads
+
+
+def test_stop_request_ends_an_unbounded_sequence(libs):
+    host, stub = libs
+    host.pb_reset()
+    stub.stub_install()
+    stub.stub_record(1 << 16)
+    s = _seq(_cfg(delay=0))
+    threading.Timer(0.5, host.pb_request_stop).start()
+    t0 = time.perf_counter()
+    host.seq_send(b"lo", s.c, 1, _cmd(host, gpu_batch=50000))
+    dt = time.perf_counter() - t0
+    assert dt < 2.5
+    p = C.c_uint64()
+    host.pb_sequence_totals(0, C.byref(p), None)
+    assert p.value > 0
+
+
+def test_tx_accounting_and_stats_line(libs, capfd):
+    host, _ = libs
+    cfg = _cfg(maxpckts=9000, delay=0, track=1, threads=2)
+    r = _run(libs, cfg, gpu_batch=2500)
+    d, c, w = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    host.pb_sequence_tx_stats(0, C.byref(d), C.byref(c), C.byref(w))
+    assert d.value == 9000 and c.value == 9000 and w.value > 0
+    # the reference's end-of-run lines (sequence.c:786-815) through a config
+    class Cfg(C.Structure):
+        _fields_ = [("interface", C.c_char_p), ("seq", SequenceT * 256)]
+
+    conf = Cfg()
+    conf.seq[0] = r["seq"].c
+    capfd.readouterr()
+    host.pb_shutdown_stats(C.byref(conf))
+    out = capfd.readouterr().out
+    assert "Completed 1 sequences!" in out
+    assert "[1] Completed sequence with a total of 9000 packets and 576000 bytes." in out
+
+
+def test_non_blocking_sequences_run_concurrently(libs):
+    """block = 0: seq_send returns after starting the threads; the reference joins
+    only when block is set or for the last sequence (sequence.c:765)."""
+    host, stub = libs
+    host.pb_reset()
+    stub.stub_install()
+    stub.stub_record(1 << 16)
+    a = _seq(_cfg(maxpckts=5000, delay=200, block=0))
+    b = _seq(_cfg(maxpckts=5000, delay=0, block=1))
+    t0 = time.perf_counter()
+    host.seq_send(b"lo", a.c, 3, _cmd(host, gpu_batch=1000))
+    t_first = time.perf_counter() - t0
+    host.seq_send(b"lo", b.c, 3, _cmd(host, gpu_batch=1000))
+    host.pb_shutdown_stats(None)
+    p0, p1 = C.c_uint64(), C.c_uint64()
+    host.pb_sequence_totals(0, C.byref(p0), None)
+    host.pb_sequence_totals(1, C.byref(p1), None)
+    assert t_first < 0.5
+    assert p1.value == 5000 and 0 < p0.value <= 5000
