@@ -1,7 +1,8 @@
 """End-to-end host pipeline rate of pcktbatch-gpu with the in-memory TX ring
 (build on the GPU -> land in pinned UMEM slots -> TX descriptors -> completions),
-no pcap: frames per second over the whole process run (startup included) and
-over the sequence (its own Average PPS line).  One JSON line per case."""
+no pcap.  Each case runs at N and 4N frames: the steady-state rate is the slope
+3N / (t(4N) - t(N)), which cancels process start and GPU initialisation; the
+whole-run rate of the 4N run is reported beside it.  One JSON line per case."""
 import json
 import os
 import re
@@ -14,21 +15,31 @@ BIN = os.path.join(ROOT, "pb-af-xdp_amd", "bin", "pcktbatch-gpu")
 BASE = ["-z", "--interface", "pbnodev0", "--smac", "52:54:00:59:29:cc", "--dmac", "52:54:00:d5:50:54",
         "--dip", "10.60.0.195", "--sip", "10.20.0.0/16", "--protocol", "udp", "--udport", "27015",
         "--delay", "0", "--track", "1"]
-CASES = [("udp64", 22, 22, 1 << 25), ("udp1500", 1458, 1458, 1 << 22), ("var64-1500", 64, 1500, 1 << 23)]
+CASES = [("udp64", 22, 22, 1 << 24), ("udp1500", 1458, 1458, 1 << 21), ("var64-1500", 64, 1500, 1 << 22)]
 env = dict(os.environ, PB_SEQ_GAP_MS="0")
+
+
+def run(lo, hi, n, threads, batch):
+    cmd = [BIN] + BASE + ["--pmin", str(lo), "--pmax", str(hi), "--maxpckts", str(n), "--threads", str(threads),
+                          "--gpubatch", str(batch)]
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    dt = time.perf_counter() - t0
+    if r.returncode:
+        print(r.stderr[-2000:], file=sys.stderr)
+        sys.exit(1)
+    m = re.search(r"total of (\d+) packets and (\d+) bytes", r.stdout)
+    return int(m.group(1)), int(m.group(2)), dt
+
+
 for name, lo, hi, n in CASES:
     for threads in (1, 2, 4):
         for batch in ([1 << 18, 1 << 20] if threads == 1 else [1 << 18]):
-            cmd = [BIN] + BASE + ["--pmin", str(lo), "--pmax", str(hi), "--maxpckts", str(n), "--threads",
-                                  str(threads), "--gpubatch", str(batch)]
-            t0 = time.perf_counter()
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
-            dt = time.perf_counter() - t0
-            if r.returncode:
-                print(r.stderr[-2000:], file=sys.stderr)
-                sys.exit(1)
-            m = re.search(r"total of (\d+) packets and (\d+) bytes", r.stdout)
-            pk, by = int(m.group(1)), int(m.group(2))
-            print(json.dumps({"case": name, "threads": threads, "gpubatch": batch, "packets": pk, "bytes": by,
-                              "wall_s": round(dt, 3), "mpps": round(pk / dt / 1e6, 1),
-                              "frame_gbps": round(by / dt / 1e9, 2)}), flush=True)
+            p1, b1, t1 = run(lo, hi, n, threads, batch)
+            p4, b4, t4 = run(lo, hi, 4 * n, threads, batch)
+            slope = t4 - t1
+            print(json.dumps({"case": name, "threads": threads, "gpubatch": batch, "packets": [p1, p4],
+                              "wall_s": [round(t1, 3), round(t4, 3)],
+                              "steady_mpps": round((p4 - p1) / slope / 1e6, 1),
+                              "steady_frame_gbps": round((b4 - b1) / slope / 1e9, 2),
+                              "whole_run_mpps": round(p4 / t4 / 1e6, 1)}), flush=True)
