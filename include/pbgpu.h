@@ -119,6 +119,13 @@ int pbgpu_copy_offsets(pbgpu_ctx *ctx, const pbgpu_frames *frames, uint64_t *hos
  * refused (-EINVAL). */
 int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *frames, void *umem, uint32_t slot_stride,
                        uint32_t first_slot, uint64_t first_frame, uint32_t n, uint16_t *lens_out);
+/* The same, asynchronous: returns once the landing is queued (registered UMEM;
+ * unregistered memory lands synchronously).  lens_out must stay valid until
+ * pbgpu_land_wait() returns for it: that call waits until at most `keep`
+ * landings are still queued, oldest first, and fills their lens_out. */
+int pbgpu_copy_to_umem_async(pbgpu_ctx *ctx, const pbgpu_frames *frames, void *umem, uint32_t slot_stride,
+                             uint32_t first_slot, uint64_t first_frame, uint32_t n, uint16_t *lens_out);
+int pbgpu_land_wait(pbgpu_ctx *ctx, uint32_t keep);
 int pbgpu_host_register(pbgpu_ctx *ctx, void *ptr, size_t bytes);
 int pbgpu_host_unregister(pbgpu_ctx *ctx, void *ptr);
 

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <deque>
 #include <vector>
 
 #include "../../include/pbgpu.h"
@@ -106,10 +107,28 @@ struct pbgpu_ctx
     timing_pair span = {nullptr, nullptr}; // PBGPU_TIMING_SPAN: first-launch / call events
     uint32_t span_n = 0;                    // launches in the open span (0: none open)
     uint8_t *h_stage = nullptr;
-    uint16_t *d_lens = nullptr; // copy_to_umem: frame lengths of the mapped scatter (device)
+    uint16_t *d_lens = nullptr; // landing: frame lengths of the mapped scatter (device), a ring
     uint16_t *h_lens = nullptr; // ... and their pinned host copy
     uint32_t lens_cap = 0;
+    uint32_t lens_head = 0;     // next free entry of the ring
     size_t h_stage_bytes = 0;
+    struct land_op
+    {
+        hipEvent_t ev;
+        uint16_t *lens_out;
+        uint32_t n;
+        uint32_t lens_off; // variable length: entries [lens_off, lens_off + n) of the lens ring
+        uint32_t fixed_len;
+    };
+    std::deque<land_op> landings;      // queued, not yet waited for (FIFO)
+    std::vector<hipEvent_t> land_pool; // recycled landing events
+    struct reg
+    {
+        uint8_t *host;
+        size_t bytes;
+        uint8_t *dev;
+    };
+    std::vector<reg> regs; // pbgpu_host_register'ed ranges and their device addresses
 };
 
 namespace
@@ -385,6 +404,9 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipStreamSynchronize(ctx->stream);
     if (ctx->land_stream)
         (void)hipStreamSynchronize(ctx->land_stream);
+    (void)pbgpu_land_wait(ctx, 0);
+    for (hipEvent_t e : ctx->land_pool)
+        (void)hipEventDestroy(e);
     for (auto &s : ctx->seqs)
         slot_free(s);
     for (auto &p : ctx->pending)
@@ -945,6 +967,7 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
     if (ctx)
     {
         (void)hipSetDevice(ctx->device);
+        (void)pbgpu_land_wait(ctx, 0);
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamSynchronize(ctx->land_stream);
     }
@@ -1195,6 +1218,10 @@ int pbgpu_host_register(pbgpu_ctx *ctx, void *ptr, size_t bytes)
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+    void *dev = NULL;
+    if (hipHostGetDevicePointer(&dev, ptr, 0) == hipSuccess && dev != NULL)
+        ctx->regs.push_back({(uint8_t *)ptr, bytes, (uint8_t *)dev});
+    (void)hipGetLastError();
     return PBGPU_OK;
 }
 
@@ -1203,91 +1230,77 @@ int pbgpu_host_unregister(pbgpu_ctx *ctx, void *ptr)
     if (ctx == NULL || ptr == NULL)
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
+    int rc = pbgpu_land_wait(ctx, 0);
+    if (rc != PBGPU_OK)
+        return rc;
+    for (size_t i = 0; i < ctx->regs.size(); ++i)
+        if (ctx->regs[i].host == (uint8_t *)ptr)
+        {
+            ctx->regs.erase(ctx->regs.begin() + (long)i);
+            break;
+        }
     HIPCHK(hipHostUnregister(ptr));
     return PBGPU_OK;
 }
 
-// send_packet()'s memcpy into UMEM slot idx * FRAME_SIZE, af_xdp.c:200-214
-int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32_t slot_stride, uint32_t first_slot,
-                       uint64_t first_frame, uint32_t n, uint16_t *lens_out)
+// device address of [p, p + n) in a registered (mapped) range, or NULL
+static uint8_t *mapped(pbgpu_ctx *ctx, uint8_t *p, uint64_t n)
 {
-    if (ctx == NULL || f == NULL || umem == NULL || slot_stride == 0 || first_frame + n > f->n_frames)
+    if (getenv("PBGPU_UMEM_DMA"))
+        return NULL;
+    for (const auto &r : ctx->regs)
+        if (p >= r.host && p + n <= r.host + r.bytes)
+            return r.dev + (p - r.host);
+    void *dev = NULL; // registered outside this context
+    if (hipHostGetDevicePointer(&dev, p, 0) == hipSuccess && dev != NULL)
+        return (uint8_t *)dev;
+    (void)hipGetLastError();
+    return NULL;
+}
+
+int pbgpu_land_wait(pbgpu_ctx *ctx, uint32_t keep)
+{
+    if (ctx == NULL)
         return PBGPU_EINVAL;
-    if (n == 0)
-        return PBGPU_OK;
-    HIPCHK(hipSetDevice(ctx->device));
-    // the landing stream waits for the build of these frames only: a build queued
-    // after it (the caller's next batch) keeps running meanwhile
+    while (ctx->landings.size() > keep)
+    {
+        pbgpu_ctx::land_op op = ctx->landings.front();
+        const hipError_t e = hipEventSynchronize(op.ev);
+        ctx->landings.pop_front();
+        ctx->land_pool.push_back(op.ev);
+        if (e != hipSuccess)
+            return PBGPU_EIO;
+        if (op.lens_out)
+        {
+            if (op.fixed_len)
+                for (uint32_t i = 0; i < op.n; ++i)
+                    op.lens_out[i] = (uint16_t)op.fixed_len;
+            else
+                memcpy(op.lens_out, ctx->h_lens + op.lens_off, (size_t)op.n * 2);
+        }
+    }
+    return PBGPU_OK;
+}
+
+// Landing into memory that is not registered with HIP: the queued landings
+// first (in order), then a strided DMA (fixed length) or a pinned staging copy.
+static int land_unmapped(pbgpu_ctx *ctx, const pbgpu_frames *f, uint8_t *dst, uint32_t slot_stride,
+                         uint64_t first_frame, uint32_t n, uint16_t *lens_out)
+{
+    int rc = pbgpu_land_wait(ctx, 0);
+    if (rc != PBGPU_OK)
+        return rc;
     hipStream_t ls = ctx->land_stream;
-    ctx->land_events = true;
-    if (f->reserved)
-        HIPCHK(hipStreamWaitEvent(ls, (hipEvent_t)f->reserved, 0));
-    else
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-    uint8_t *dst = (uint8_t *)umem + (uint64_t)first_slot * slot_stride;
     if (f->fixed_len)
     {
-        if (f->fixed_len > slot_stride)
-            return PBGPU_EINVAL;
-        // registered (mapped) UMEM: the GPU stores each frame into its slot over the host
-        // link; otherwise a strided DMA copy (one row per frame)
-        void *dev_dst = NULL;
-        if (hipHostGetDevicePointer(&dev_dst, dst, 0) == hipSuccess && dev_dst != NULL &&
-            !getenv("PBGPU_UMEM_DMA"))
-            HIPCHK(pbk_launch_scatter_fixed(f->data + first_frame * f->fixed_len, f->fixed_len, n, (uint8_t *)dev_dst,
-                                            slot_stride, ls));
-        else
-        {
-            (void)hipGetLastError();
-            HIPCHK(hipMemcpy2DAsync(dst, slot_stride, f->data + first_frame * f->fixed_len, f->fixed_len,
-                                    f->fixed_len, n, hipMemcpyDeviceToHost, ls));
-        }
+        HIPCHK(hipMemcpy2DAsync(dst, slot_stride, f->data + first_frame * f->fixed_len, f->fixed_len, f->fixed_len,
+                                n, hipMemcpyDeviceToHost, ls));
         HIPCHK(hipStreamSynchronize(ls));
         if (lens_out)
             for (uint32_t i = 0; i < n; ++i)
                 lens_out[i] = (uint16_t)f->fixed_len;
         return PBGPU_OK;
     }
-    // variable length: a scatter kernel writes straight into registered
-    // (mapped) UMEM; unregistered memory goes through a pinned staging copy.
-    // A frame longer than a slot would overrun the next slot (or, in the last
-    // slot, the UMEM allocation): refused up front from the sequence's longest
-    // frame, as the fixed-length path refuses fixed_len > slot_stride (the
-    // reference does not check, af_xdp.c:214).
-    if (f->seq_idx >= PB_MAX_SEQUENCES || !ctx->seqs[f->seq_idx].loaded)
-        return PBGPU_EINVAL;
-    if (ctx->seqs[f->seq_idx].max_flen > slot_stride)
-        return PBGPU_EINVAL;
-    void *dev_dst = NULL;
-    uint16_t *d_lens = NULL;
-    if (hipHostGetDevicePointer(&dev_dst, dst, 0) == hipSuccess && dev_dst != NULL)
-    {
-        // lengths go through buffers owned by the context (device + pinned host),
-        // never through a stream-ordered allocation or a pageable async copy
-        if (ctx->lens_cap < n)
-        {
-            HIPCHK(hipStreamSynchronize(ls));
-            if (ctx->d_lens)
-                (void)hipFree(ctx->d_lens);
-            if (ctx->h_lens)
-                (void)hipHostFree(ctx->h_lens);
-            ctx->d_lens = NULL;
-            ctx->h_lens = NULL;
-            ctx->lens_cap = 0;
-            HIPCHK(hipMalloc((void **)&ctx->d_lens, (size_t)n * 2));
-            HIPCHK(hipHostMalloc((void **)&ctx->h_lens, (size_t)n * 2, 0));
-            ctx->lens_cap = n;
-        }
-        d_lens = ctx->d_lens;
-        HIPCHK(pbk_launch_scatter(f->data, f->offsets, first_frame, n, (uint8_t *)dev_dst, slot_stride, d_lens,
-                                  ls));
-        HIPCHK(hipMemcpyAsync(ctx->h_lens, d_lens, (size_t)n * 2, hipMemcpyDeviceToHost, ls));
-        HIPCHK(hipStreamSynchronize(ls));
-        if (lens_out)
-            memcpy(lens_out, ctx->h_lens, (size_t)n * 2);
-        return PBGPU_OK;
-    }
-    (void)hipGetLastError();
     std::vector<uint64_t> off(n + 1);
     HIPCHK(hipMemcpyAsync(off.data(), f->offsets + first_frame, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
                           ls));
@@ -1314,6 +1327,104 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
             lens_out[i] = (uint16_t)len;
     }
     return PBGPU_OK;
+}
+
+// send_packet()'s memcpy into UMEM slot idx * FRAME_SIZE, af_xdp.c:200-214.
+// Registered (mapped) UMEM: a scatter kernel on the landing stream stores each
+// frame into its slot over the host link, queued behind the build of these
+// frames only; the caller waits with pbgpu_land_wait (several landings may be
+// in flight: their launch and completion latencies overlap).  Unregistered
+// memory: a synchronous strided DMA (fixed length) or pinned staging copy.
+int pbgpu_copy_to_umem_async(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32_t slot_stride,
+                             uint32_t first_slot, uint64_t first_frame, uint32_t n, uint16_t *lens_out)
+{
+    if (ctx == NULL || f == NULL || umem == NULL || slot_stride == 0 || first_frame + n > f->n_frames)
+        return PBGPU_EINVAL;
+    if (n == 0)
+        return PBGPU_OK;
+    // a frame longer than a slot would overrun the next slot (or, in the last slot,
+    // the UMEM allocation): refused, from the fixed length or the sequence's
+    // longest frame (the reference does not check, af_xdp.c:214)
+    if (f->fixed_len ? f->fixed_len > slot_stride
+                     : (f->seq_idx >= PB_MAX_SEQUENCES || !ctx->seqs[f->seq_idx].loaded ||
+                        ctx->seqs[f->seq_idx].max_flen > slot_stride))
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t ls = ctx->land_stream;
+    ctx->land_events = true;
+    if (f->reserved)
+        HIPCHK(hipStreamWaitEvent(ls, (hipEvent_t)f->reserved, 0));
+    else
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    uint8_t *dst = (uint8_t *)umem + (uint64_t)first_slot * slot_stride;
+    uint8_t *dev_dst = mapped(ctx, dst, (uint64_t)n * slot_stride);
+    if (dev_dst == NULL)
+        return land_unmapped(ctx, f, dst, slot_stride, first_frame, n, lens_out);
+    pbgpu_ctx::land_op op = {nullptr, lens_out, n, 0, f->fixed_len};
+    if (f->fixed_len)
+        HIPCHK(pbk_launch_scatter_fixed(f->data + first_frame * f->fixed_len, f->fixed_len, n, dev_dst, slot_stride,
+                                        ls));
+    else
+    {
+        // lengths: a contiguous range of the context's ring (device + pinned host), FIFO
+        // with the queued landings; never a stream-ordered allocation or a pageable copy
+        if (ctx->lens_cap < n)
+        {
+            int rc = pbgpu_land_wait(ctx, 0);
+            if (rc != PBGPU_OK)
+                return rc;
+            HIPCHK(hipStreamSynchronize(ls));
+            if (ctx->d_lens)
+                (void)hipFree(ctx->d_lens);
+            if (ctx->h_lens)
+                (void)hipHostFree(ctx->h_lens);
+            ctx->d_lens = NULL;
+            ctx->h_lens = NULL;
+            ctx->lens_cap = 0;
+            const uint32_t cap = n > (1u << 16) ? n : (1u << 16);
+            HIPCHK(hipMalloc((void **)&ctx->d_lens, (size_t)cap * 2));
+            HIPCHK(hipHostMalloc((void **)&ctx->h_lens, (size_t)cap * 2, 0));
+            ctx->lens_cap = cap;
+            ctx->lens_head = 0;
+        }
+        uint32_t off = ctx->lens_head + n <= ctx->lens_cap ? ctx->lens_head : 0;
+        // wait for the queued landings whose ranges the new one would overwrite
+        for (;;)
+        {
+            bool clash = false;
+            for (const auto &q : ctx->landings)
+                if (!q.fixed_len && q.lens_off < off + n && off < q.lens_off + q.n)
+                    clash = true;
+            if (!clash)
+                break;
+            int rc = pbgpu_land_wait(ctx, (uint32_t)ctx->landings.size() - 1);
+            if (rc != PBGPU_OK)
+                return rc;
+        }
+        HIPCHK(pbk_launch_scatter(f->data, f->offsets, first_frame, n, dev_dst, slot_stride, ctx->d_lens + off, ls));
+        HIPCHK(hipMemcpyAsync(ctx->h_lens + off, ctx->d_lens + off, (size_t)n * 2, hipMemcpyDeviceToHost, ls));
+        op.lens_off = off;
+        ctx->lens_head = off + n;
+    }
+    if (!ctx->land_pool.empty())
+    {
+        op.ev = ctx->land_pool.back();
+        ctx->land_pool.pop_back();
+    }
+    else
+        HIPCHK(hipEventCreateWithFlags(&op.ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(op.ev, ls));
+    ctx->landings.push_back(op);
+    return PBGPU_OK;
+}
+
+int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32_t slot_stride, uint32_t first_slot,
+                       uint64_t first_frame, uint32_t n, uint16_t *lens_out)
+{
+    int rc = pbgpu_copy_to_umem_async(ctx, f, umem, slot_stride, first_slot, first_frame, n, lens_out);
+    if (rc == PBGPU_OK)
+        rc = pbgpu_land_wait(ctx, 0);
+    return rc;
 }
 
 int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)

@@ -1553,6 +1553,8 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         // window's longest frames (s_ord is longest first) take 32 / 16 lanes: y frames of
         // 32, then x of 16, then 8 each, groups aligned to their size
         uint32_t g = G, grp0 = tid / G, lg = tid % G;
+        // the layout's counts assume 256 lanes: 32 y + 16 x == 256 for 9-16 frames, 32 F <= 256 for F <= 8
+        static_assert(PB_WG == 256, "pb_vstage_kernel's 32/16/8-lane window layout is for 256-thread workgroups");
         if (G == 8 && !(K.fst_dbg & 16u))
         {
             const uint32_t F = se - sb;

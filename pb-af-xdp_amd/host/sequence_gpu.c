@@ -27,6 +27,8 @@
 #include <unistd.h>
 
 #define PB_MAX_WORKERS 1024
+#define PB_LAND_INFLIGHT 3 /* landings queued per thread */
+#define PB_LAND_CHUNK 1024 /* frames per landing (a quarter of the UMEM) */
 #define PB_BATCH_BYTES_MAX (256ull << 20) /* device bytes per frame buffer (two per worker) */
 
 static uint64_t total_pckts[PB_MAX_SEQUENCES];
@@ -130,7 +132,11 @@ static uint64_t gb_n_frames(void *frames)
 static int gb_land(void *h, void *frames, uint8_t *umem, uint32_t stride, uint32_t slot, uint64_t first, uint32_t n,
                    uint16_t *lens)
 {
-    return pbgpu_copy_to_umem((pbgpu_ctx *)h, (pbgpu_frames *)frames, umem, stride, slot, first, n, lens);
+    return pbgpu_copy_to_umem_async((pbgpu_ctx *)h, (pbgpu_frames *)frames, umem, stride, slot, first, n, lens);
+}
+static int gb_land_wait(void *h, uint32_t keep)
+{
+    return pbgpu_land_wait((pbgpu_ctx *)h, keep);
 }
 static int gb_reg(void *h, void *p, size_t n)
 {
@@ -149,8 +155,8 @@ static void gb_close(void *h)
     pbgpu_close((pbgpu_ctx *)h);
 }
 
-static const pb_builder_t gpu_builder = {gb_open, gb_load, gb_alloc, gb_build, gb_n_frames, gb_land,
-                                         gb_reg,  gb_unreg, gb_free, gb_close};
+static const pb_builder_t gpu_builder = {gb_open, gb_load,  gb_alloc, gb_build, gb_n_frames, gb_land,
+                                         gb_land_wait, gb_reg, gb_unreg, gb_free, gb_close};
 static const pb_builder_t *builder = &gpu_builder;
 
 void pb_set_builder(const pb_builder_t *b)
@@ -381,31 +387,63 @@ static void *gpu_worker(void *p)
             break;
         }
         const uint64_t nf = B->n_frames(fr[cur]);
-        uint64_t f0 = 0;
+        /* land in slot-ring order with up to PB_LAND_INFLIGHT landings queued: chunk
+         * c + 1 lands while chunk c is submitted (their latencies overlap) */
+        uint64_t f0 = 0, f_issue = 0;
+        uint32_t land_slot = xsk.next_slot, in_land = 0;
+        uint32_t qn_[PB_LAND_INFLIGHT];
+        int qh = 0, qn = 0;
         while (f0 < nf && !done && !stop_requested)
         {
-            /* land as many frames as free UMEM slots allow, in slot-ring order */
-            while (pb_xsk_free_slots(&xsk) == 0 && !stop_requested)
-                if (pb_xsk_complete(&xsk, PB_NUM_FRAMES) == 0)
-                    sched_yield();
-            if (stop_requested)
-                break;
-            uint32_t n = pb_xsk_free_slots(&xsk);
-            if ((uint64_t)n > nf - f0)
-                n = (uint32_t)(nf - f0);
-            const uint32_t slot = xsk.next_slot;
-            const uint32_t n1 = n < PB_NUM_FRAMES - slot ? n : PB_NUM_FRAMES - slot; /* the slot ring wraps */
-            if ((rc = B->land(ctx, fr[cur], umem, PB_FRAME_SIZE, slot, f0, n1, lens)) != 0 ||
-                (n1 < n && (rc = B->land(ctx, fr[cur], umem, PB_FRAME_SIZE, 0, f0 + n1, n - n1, lens + n1)) != 0))
+            while (qn < PB_LAND_INFLIGHT && f_issue < nf)
             {
-                fprintf(stderr, "[%d] Error landing frames from GPU %d :: %s.\n", seq_num, w->gpu, pbgpu_strerror(rc));
+                uint32_t free_slots = pb_xsk_free_slots(&xsk) - in_land;
+                if (free_slots == 0)
+                {
+                    if (qn)
+                        break;
+                    if (pb_xsk_complete(&xsk, PB_NUM_FRAMES) == 0)
+                        sched_yield();
+                    if (stop_requested)
+                        break;
+                    continue;
+                }
+                uint32_t n = free_slots < PB_LAND_CHUNK ? free_slots : PB_LAND_CHUNK;
+                if ((uint64_t)n > nf - f_issue)
+                    n = (uint32_t)(nf - f_issue);
+                if (n > PB_NUM_FRAMES - land_slot) /* the slot ring wraps: a chunk never does */
+                    n = PB_NUM_FRAMES - land_slot;
+                if ((rc = B->land(ctx, fr[cur], umem, PB_FRAME_SIZE, land_slot, f_issue, n, lens + land_slot)) != 0)
+                {
+                    fprintf(stderr, "[%d] Error landing frames from GPU %d :: %s.\n", seq_num, w->gpu,
+                            pbgpu_strerror(rc));
+                    last_error = rc;
+                    done = 3;
+                    break;
+                }
+                qn_[(qh + qn) % PB_LAND_INFLIGHT] = n;
+                ++qn;
+                in_land += n;
+                land_slot = (land_slot + n) & (PB_NUM_FRAMES - 1);
+                f_issue += n;
+            }
+            if (done || qn == 0)
+                break;
+            /* the oldest landing is in its slots: submit it */
+            if ((rc = B->land_wait(ctx, (uint32_t)qn - 1)) != 0)
+            {
                 last_error = rc;
                 done = 3;
                 break;
             }
+            uint32_t n = qn_[qh];
+            qh = (qh + 1) % PB_LAND_INFLIGHT;
+            --qn;
+            in_land -= n;
+            const uint16_t *ln = lens + xsk.next_slot;
             uint64_t bytes = 0;
             for (uint32_t i = 0; i < n; ++i)
-                bytes += lens[i];
+                bytes += ln[i];
             if (seq->max_bytes > 0) /* send until the total reaches max_bytes (sequence.c:668-674) */
             {
                 uint64_t tot = __atomic_load_n(&total_bytes[w->seq_idx], __ATOMIC_RELAXED);
@@ -419,7 +457,7 @@ static void *gpu_worker(void *p)
                     uint32_t m = 0;
                     uint64_t b = 0;
                     while (m < n && tot + b < seq->max_bytes)
-                        b += lens[m++];
+                        b += ln[m++];
                     if (__atomic_compare_exchange_n(&total_bytes[w->seq_idx], &tot, tot + b, 0, __ATOMIC_RELAXED,
                                                     __ATOMIC_RELAXED))
                     {
@@ -435,7 +473,7 @@ static void *gpu_worker(void *p)
             }
             else
                 __atomic_add_fetch(&total_bytes[w->seq_idx], bytes, __ATOMIC_RELAXED);
-            if ((rc = pb_xsk_send(&xsk, lens, n)) != 0)
+            if ((rc = pb_xsk_send(&xsk, ln, n)) != 0)
             {
                 fprintf(stderr, "[%d][%d] ERROR - Could not send packet on AF_XDP socket (%d) :: %s.\n", seq_num, 1,
                         w->shard, strerror(-rc));
@@ -468,6 +506,8 @@ static void *gpu_worker(void *p)
             if (seq->time > 0 && now_s() - t0 >= (double)seq->time)
                 done = 2;
         }
+        /* a stop leaves landings queued: let them finish before the buffers are reused */
+        (void)B->land_wait(ctx, 0);
         if (verbose)
             fprintf(stdout, "[%d] Thread %d (GPU %d) sent %llu frames of iteration batch %llu.\n", seq_num, w->shard,
                     w->gpu, (unsigned long long)f0, (unsigned long long)step);

@@ -72,9 +72,11 @@ typedef struct pb_builder
     /* asynchronous; the frames are ready for land() */
     int (*build)(void *h, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, void *frames);
     uint64_t (*n_frames)(void *frames);
-    /* frames [first, first + n) -> slots first_slot.. of `umem` (stride bytes apart), lengths to lens */
+    /* queue frames [first, first + n) -> slots first_slot.. of `umem` (stride bytes apart),
+     * lengths to lens once land_wait(keep) has left at most `keep` landings queued */
     int (*land)(void *h, void *frames, uint8_t *umem, uint32_t stride, uint32_t first_slot, uint64_t first,
                 uint32_t n, uint16_t *lens);
+    int (*land_wait)(void *h, uint32_t keep);
     int (*host_register)(void *h, void *p, size_t n);
     int (*host_unregister)(void *h, void *p);
     void (*free_frames)(void *h, void *frames);

@@ -126,6 +126,12 @@ static int s_land(void *h, void *frames, uint8_t *umem, uint32_t stride, uint32_
     return 0;
 }
 
+static int s_land_wait(void *h, uint32_t keep)
+{
+    (void)h, (void)keep; /* s_land is synchronous */
+    return 0;
+}
+
 static int s_reg(void *h, void *p, size_t n)
 {
     (void)h, (void)p, (void)n;
@@ -148,7 +154,8 @@ static void s_close(void *h)
     free(h);
 }
 
-static const pb_builder_t stub = {s_open, s_load, s_alloc, s_build, s_n_frames, s_land, s_reg, s_unreg, s_free, s_close};
+static const pb_builder_t stub = {s_open,  s_load,   s_alloc, s_build, s_n_frames, s_land,
+                                  s_land_wait, s_reg, s_unreg, s_free, s_close};
 
 void stub_install(void)
 {

@@ -41,6 +41,14 @@ SHAPES = [
      ("pb_vstage_kernel<64", "pb_stage_kernel<64", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("vstage_g32_wgf7", {"PBGPU_G": "32", "PBGPU_WGF": "7"},
      ("pb_vstage_kernel<32", "pb_stage_kernel<32", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
+    # pb_vstage_kernel's lane layouts by window: fixed 8-lane groups (bit 4) and
+    # no 32-lane groups (bit 5) build the same bytes as the default 32/16/8 layout
+    ("vstage_fixed8", {"PBGPU_FST_DBG": "16"},
+     ("pb_vstage_kernel<8", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
+      "pb_xpage_kernel", "pb_gpf_kernel")),
+    ("vstage_no32", {"PBGPU_FST_DBG": "32"},
+     ("pb_vstage_kernel<8", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
+      "pb_xpage_kernel", "pb_gpf_kernel")),
 ]
 
 # pb_fstage_kernel shapes (fixed lengths > 128 B, multiple of 4, random payload)
@@ -95,7 +103,8 @@ def test_kernel_shape_matches_oracle(ctx, monkeypatch, shape, env, kernels, name
     assert kern.startswith(kernels), kern
 
 
-@pytest.mark.parametrize("shape,env,kernels", SHAPES[:1] + SHAPES[2:3], ids=["gpf", "stage_g8_wgf5"])
+@pytest.mark.parametrize("shape,env,kernels", [s for s in SHAPES if s[0] in ("gpf", "stage_g8_wgf5")],
+                         ids=["gpf", "stage_g8_wgf5"])
 @pytest.mark.parametrize("name,rule,fold", pc.RULE_CASES)
 def test_kernel_shape_rules(ctx, monkeypatch, shape, env, kernels, name, rule, fold):
     for k, v in env.items():

@@ -1,6 +1,7 @@
 """GPU parity: libpbgpu.so (the HIP kernels, through the C ABI) against the
 committed golden vectors and the CPU oracle, bit-exact; full-size properties
 at BASELINE.json sizes.  Run on the MI355X box: pytest -m gpu."""
+import ctypes as C
 import json
 import os
 
@@ -264,3 +265,71 @@ def test_timing_modes(ctx):
     with pytest.raises(pbgpu.PbError):
         ctx.set_timing(7)
     fb.free()
+
+
+@pytest.mark.parametrize("name", ["c3_udp_var", "c2_udp_1500", "tcp_all_flags_var"])
+def test_async_landings_overlap_the_next_build(ctx, name):
+    """pbgpu_copy_to_umem_async: three landings queued into registered 4 KiB slots
+    (the second buffer building meanwhile on the build stream), waited oldest
+    first; every slot holds its frame and nothing past it (af_xdp.c:211-214)."""
+    seq = Sequence.from_config(pc.get(name))
+    ctx.load_sequence(10, seq, pc.SEED_BASE)
+    n = 3000
+    a = ctx.alloc_frames(*ctx.build_size(10, n))
+    b = ctx.alloc_frames(*ctx.build_size(10, n))
+    umem = np.full(4096 * 4096, 0xEE, dtype=np.uint8)
+    assert ctx.lib.pbgpu_host_register(ctx.h, umem.ctypes.data, umem.nbytes) == 0
+    lens = np.zeros(4096, dtype=np.uint16)
+    L = ctx.lib
+    L.pbgpu_copy_to_umem_async.argtypes = [C.c_void_p, C.POINTER(pbgpu.Frames), C.c_void_p, C.c_uint32, C.c_uint32,
+                                           C.c_uint64, C.c_uint32, C.c_void_p]
+    L.pbgpu_land_wait.argtypes = [C.c_void_p, C.c_uint32]
+    try:
+        ctx.build(10, 7, n, a)
+        # first landing of a context synchronises the build stream; later ones wait on events
+        assert L.pbgpu_copy_to_umem_async(ctx.h, a.ptr, umem.ctypes.data, 4096, 0, 0, 100, lens.ctypes.data) == 0
+        assert L.pbgpu_land_wait(ctx.h, 0) == 0
+        ctx.build(10, 7 + n, n, b)  # queued behind nothing the landings wait for
+        chunks = [(100, 1000, 1500), (1600, 2500, 500), (3600, 0, 496)]  # (slot, first frame, count)
+        for slot, first, cnt in chunks:
+            assert L.pbgpu_copy_to_umem_async(ctx.h, a.ptr, umem.ctypes.data, 4096, slot, first, cnt,
+                                              lens[slot:].ctypes.data) == 0
+        assert L.pbgpu_land_wait(ctx.h, 2) == 0 and L.pbgpu_land_wait(ctx.h, 0) == 0
+        ctx.sync()
+    finally:
+        L.pbgpu_host_unregister(ctx.h, umem.ctypes.data)
+    want_a = ob.frames(seq, 10, 7, n, pc.SEED_BASE)
+    want_b = ob.frames(seq, 10, 7 + n, n, pc.SEED_BASE)
+    slots = umem.reshape(4096, 4096)
+    for slot, first, cnt in [(0, 0, 100)] + chunks:
+        for j in range(cnt):
+            f = want_a[first + j]
+            assert int(lens[slot + j]) == len(f)
+            assert slots[slot + j, :len(f)].tobytes() == f
+            assert (slots[slot + j, len(f):] == 0xEE).all()
+    assert b.frames() == want_b
+    a.free()
+    b.free()
+
+
+def test_jumbo_frames_refused_by_4k_slots(ctx):
+    """A frame longer than its UMEM slot is refused (-EINVAL), registered or not,
+    fixed or variable length: nothing is written past a slot."""
+    for name in ("udp_jumbo_var", "udp_jumbo_fixed_odd"):
+        seq = Sequence.from_config(pc.get(name))
+        ctx.load_sequence(11, seq, pc.SEED_BASE)
+        fb = ctx.alloc_frames(*ctx.build_size(11, 64))
+        ctx.build(11, 0, 64, fb)
+        ctx.sync()
+        umem = np.full(4096 * 64, 0xEE, dtype=np.uint8)
+        lens = np.zeros(64, dtype=np.uint16)
+        for registered in (True, False):
+            if registered:
+                assert ctx.lib.pbgpu_host_register(ctx.h, umem.ctypes.data, umem.nbytes) == 0
+            rc = ctx.lib.pbgpu_copy_to_umem(ctx.h, fb.ptr, umem.ctypes.data, 4096, 0, 0, 64,
+                                            lens.ctypes.data_as(C.POINTER(C.c_uint16)))
+            if registered:
+                ctx.lib.pbgpu_host_unregister(ctx.h, umem.ctypes.data)
+            assert rc == -22
+            assert (umem == 0xEE).all()
+        fb.free()
