@@ -15,6 +15,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <vector>
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define CK(x)                                                                        \
@@ -209,6 +211,23 @@ __global__ __launch_bounds__(256) void fill_paced(uint8_t *dst, uint32_t ppw, ui
     }
     if (x == 0x12345678u && t == 999) // keep the chain
         lds_dummy[0] = x;
+}
+
+// Frame-owned blocks with precomputed bounds (no division in the kernel): block b
+// of 2^bs bytes writes the lines [R[b], R[b + 1]) of the frames whose first line
+// starts in it (R from the host, as fill_fown defines them), WG threads with one
+// 16-B store per lane per grid chunk of the region; mode 1 maps blocks to
+// workgroups XCD-strided.
+template <int WG>
+__global__ __launch_bounds__(WG) void fill_fown2(uint8_t *dst, const uint64_t *R, uint32_t bs, uint32_t mode, uint32_t nblk)
+{
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint32_t blk = mode ? ((b >> 3) + (b & 7u) * (nblk >> 3)) : b; // mode 1: XCD x owns a contiguous run of blocks
+    const uint64_t r0 = R[blk], r1 = R[blk + 1];
+    const uint64_t g0 = r0 & ~(uint64_t)(WG * 16 - 1);
+    for (uint64_t a = g0 + 16ull * t; a < r1; a += WG * 16)
+        if (a >= r0)
+            st16<false>(dst + a, u32x4{b, t, 2u, 3u});
 }
 
 // Strided page ownership: workgroup b writes `ppw` 4 KiB pages at a stride of S
@@ -426,6 +445,38 @@ int main(int argc, char **argv)
                 snprintf(nm, sizeof nm, "occ win %s wb=24576 nwin=4 from-lds lds=%u", mode ? "xcd" : "linear", l);
                 rep(nm, (uint64_t)grid * wb * nwin,
                     timeit([&] { hipLaunchKernelGGL(fill_win, dim3(grid), dim3(256), l, 0, buf, wb, nwin, 0u, 1u, mode); }, 10));
+            }
+    }
+    if (want(argc, argv, "fown2"))
+    {
+        for (uint32_t L : {1500u, 824u})
+            for (uint32_t bs : {12u, 13u, 14u})
+            {
+                const uint32_t nblk = (uint32_t)(((g_bytes - 65536) >> bs) / 8 * 8);
+                std::vector<uint64_t> R(nblk + 1);
+                for (uint32_t i = 0; i <= nblk; ++i)
+                {
+                    const uint64_t a = (uint64_t)i << bs;
+                    uint64_t f = a / L;
+                    while (((f * L) & ~127ull) < a)
+                        ++f;
+                    R[i] = (f * L) & ~127ull;
+                }
+                uint64_t *dR;
+                CK(hipMalloc(&dR, R.size() * 8));
+                CK(hipMemcpy(dR, R.data(), R.size() * 8, hipMemcpyHostToDevice));
+                const uint64_t bytes = R[nblk] - R[0];
+                for (uint32_t mode : {0u})
+                {
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "fown2 L=%u block=%u wg=256", L, 1u << bs);
+                    rep(nm, bytes, timeit([&] { hipLaunchKernelGGL(fill_fown2<256>, dim3(nblk), dim3(256), 0, 0, buf, dR, bs, mode, nblk); }, 20));
+                    snprintf(nm, sizeof nm, "fown2 L=%u block=%u wg=512", L, 1u << bs);
+                    rep(nm, bytes, timeit([&] { hipLaunchKernelGGL(fill_fown2<512>, dim3(nblk), dim3(512), 0, 0, buf, dR, bs, mode, nblk); }, 20));
+                    snprintf(nm, sizeof nm, "fown2 L=%u block=%u wg=1024", L, 1u << bs);
+                    rep(nm, bytes, timeit([&] { hipLaunchKernelGGL(fill_fown2<1024>, dim3(nblk), dim3(1024), 0, 0, buf, dR, bs, mode, nblk); }, 20));
+                }
+                CK(hipFree(dR));
             }
     }
     if (want(argc, argv, "stride"))
