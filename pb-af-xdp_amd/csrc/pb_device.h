@@ -133,7 +133,9 @@ struct pb_kargs
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)
 // pb_vstage_kernel's LDS besides the stage: lcg48 entries, header image + start, length, z, header
 // sum, build order per frame, window list
-#define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + (size_t)(wgf) * (16 + 5) * 4 + ((size_t)(wgf) + 2) * 4)
+// (arrays for wgf own frames + PB_VST_GHOSTS earlier frames sharing the first 128-B line)
+#define PB_VST_GHOSTS 4
+#define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + ((size_t)(wgf) + PB_VST_GHOSTS) * (16 + 5) * 4 + ((size_t)(wgf) + PB_VST_GHOSTS + 2) * 4)
 
 __device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)
 {

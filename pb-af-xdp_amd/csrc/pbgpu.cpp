@@ -855,6 +855,8 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 {
                     K.vst = 1;
                     K.fst_dbg = (uint32_t)env_int("PBGPU_FST_DBG", 0);
+                    // phase A has one lane per frame for the own frames and the ghosts
+                    K.stage_wgf = std::min<uint32_t>(K.stage_wgf, PB_WG - PB_VST_GHOSTS);
                 }
             }
             // fixed-length staged kernel (pb_fstage_kernel): lengths > 128 B that are a

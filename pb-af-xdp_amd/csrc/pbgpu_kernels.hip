@@ -1428,24 +1428,54 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     constexpr uint32_t NGW = PB_WG / G; // frames in flight per workgroup
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     const uint32_t WF = K.stage_wgf, W = K.stage_win, SB = K.stage_bytes;
+    const uint32_t CAP = WF + PB_VST_GHOSTS; // frames of the workgroup's arrays: ghosts + own
     pb_u32x4 *const stage = reinterpret_cast<pb_u32x4 *>(s_dyn);
     uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_dyn + (SB >> 2)); // lcg48[0 .. PB_STAGE_L48)
     uint32_t *const s_img = s_dyn + (SB >> 2) + 2 * PB_STAGE_L48;      // header image, 16 dwords per frame
-    uint32_t *const s_r = s_img + WF * 16;                             // frame start, workgroup-relative
-    uint32_t *const s_len = s_r + WF;
-    uint32_t *const s_z = s_len + WF;  // LCG state at the frame's first 16-B chunk
-    uint32_t *const s_hs = s_z + WF;   // header + pseudo header word sum, folded (frame alignment)
-    uint32_t *const s_win = s_hs + WF; // s_win[w]: first frame of window w, [nwin] = nfr
-    uint32_t *const s_ord = s_win + WF + 2; // frames of each window, longest first
+    uint32_t *const s_r = s_img + CAP * 16;                            // frame start, workgroup-relative
+    uint32_t *const s_len = s_r + CAP;
+    uint32_t *const s_z = s_len + CAP;  // LCG state at the frame's first 16-B chunk
+    uint32_t *const s_hs = s_z + CAP;   // header + pseudo header word sum, folded (frame alignment)
+    uint32_t *const s_win = s_hs + CAP; // s_win[w]: first frame of window w, [nwin] = nfr
+    uint32_t *const s_ord = s_win + CAP + 2; // frames of each window, longest first
 
     const uint32_t tid = threadIdx.x;
     const uint32_t flags = K.flags;
     const uint32_t hl = K.hl;
+    // Workgroup b owns frames [f0, f0 + nown) and stores exactly the output bytes
+    // [lo, hi): lo = the 128-B line holding its first frame's start (0 for b = 0), hi =
+    // the next workgroup's lo.  No line is written by two workgroups (two XCDs): an
+    // edge that split a line cost 5-12% of the write rate (profiles/r02/wbench,
+    // shift_*.txt).  The bytes of [lo, start(f0)) belong to up to PB_VST_GHOSTS earlier
+    // frames ("ghosts"), built here in full (their checksums need every byte) and
+    // stored only inside [lo, hi); the bytes of the own last frames past hi are the
+    // next workgroup's ghosts.
     const uint64_t f0 = (uint64_t)blockIdx.x * WF;
     const uint64_t left = K.n_frames - f0;
-    const uint32_t nfr = left < WF ? (uint32_t)left : WF;
-    const uint64_t W0 = K.fixed_len ? f0 * K.fixed_len : K.offsets[f0];
+    const uint32_t nown = left < WF ? (uint32_t)left : WF;
+    const uint64_t S0 = K.fixed_len ? f0 * K.fixed_len : K.offsets[f0];
+    // (PBGPU_FST_DBG bit 6, A/B only: the round-1 edges at the frame starts, lines split)
+    const uint64_t emask = (K.fst_dbg & 64u) ? ~0ull : ~127ull;
+    const uint64_t lo_abs = blockIdx.x ? (S0 & emask) : 0ull;
+    const uint64_t fe = f0 + nown;
+    const uint64_t hi_abs = fe < K.n_frames ? ((K.fixed_len ? fe * K.fixed_len : K.offsets[fe]) & emask)
+                                            : (K.fixed_len ? K.n_frames * K.fixed_len : K.offsets[K.n_frames]);
+    uint32_t ng = 0;
+    {
+        // ghost t = frame f0 - 1 - t, present while it ends (= frame f0 - t starts) past lo;
+        // lanes 0..3 of every wave test t = lane, the set bits are a prefix
+        const uint32_t l = tid & 63u;
+        bool g = false;
+        if (blockIdx.x && l < PB_VST_GHOSTS && f0 > l)
+            g = (K.fixed_len ? (f0 - l) * K.fixed_len : K.offsets[f0 - l]) > lo_abs;
+        const uint64_t m = __ballot(g);
+        ng = (uint32_t)__builtin_ctzll(~m);
+    }
+    const uint64_t fg = f0 - ng;   // the workgroup's first frame (a ghost if ng > 0)
+    const uint32_t nfr = ng + nown; // frames built
+    const uint64_t W0 = K.fixed_len ? fg * K.fixed_len : K.offsets[fg];
     const uint64_t wbase = W0 & ~15ull;
+    const uint32_t lo_rel = (uint32_t)(lo_abs - wbase), hi_rel = (uint32_t)(hi_abs - wbase);
     const uint32_t nsc = SB >> 4; // stage chunks
 
     // ---------------- A: one lane per frame; the stage starts zero ----------------
@@ -1460,7 +1490,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
     if (tid < nfr)
     {
-        const uint64_t f = f0 + tid;
+        const uint64_t f = fg + tid;
         uint64_t base;
         uint32_t flen;
         if (K.fixed_len)
@@ -1704,25 +1734,36 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         __syncthreads();
 
         // ---------------- S: stage -> HBM, contiguous 16-B stores, then zero ----------------
-        // chunks [c0, c1) whole; 0 (lo_b != 0) and c1 (hi_b % 16 != 0) are shared with the
-        // neighbouring windows and byte-masked, each by the lane that then zeroes it
-        const uint32_t lo_b = R0 - sbase, hi_b = R1 - sbase;
-        const uint32_t c0 = lo_b ? 1u : 0u, c1 = hi_b >> 4;
+        // the window's bytes [R0, R1) clipped to the workgroup's [lo, hi): whole chunks
+        // [cf0, cf1); a chunk the window shares with a neighbouring window (same
+        // workgroup) is byte-masked, stored by the lane that then zeroes it
+        const uint32_t R0c = R0 > lo_rel ? R0 : lo_rel, R1c = R1 < hi_rel ? R1 : hi_rel;
+        uint32_t cf0 = 0, cf1 = 0;
         uint8_t *const gout = K.out + wbase + sbase;
-        if (tid == 0 && lo_b)
+        if (R0c < R1c)
         {
-            const pb_u32x4 v = stage[0];
-            pb_store_chunk(gout, v[0], v[1], v[2], v[3], -(int)lo_b, (int)(hi_b - lo_b));
+            const uint32_t lo_b = R0c - sbase, hi_b = R1c - sbase;
+            const uint32_t cl = lo_b >> 4, ch = hi_b >> 4;
+            cf0 = (lo_b + 15u) >> 4;
+            cf1 = ch;
+            if ((lo_b & 15u) && tid == (cl & (PB_WG - 1u)))
+            {
+                const pb_u32x4 v = stage[cl];
+                pb_store_chunk(gout + 16 * cl, v[0], v[1], v[2], v[3], (int)(16 * cl) - (int)lo_b,
+                               (int)(hi_b - lo_b));
+            }
+            if ((hi_b & 15u) && !((lo_b & 15u) && cl == ch) && tid == (ch & (PB_WG - 1u)))
+            {
+                const pb_u32x4 v = stage[ch];
+                pb_store_chunk(gout + 16 * ch, v[0], v[1], v[2], v[3], (int)(16 * ch) - (int)lo_b,
+                               (int)(hi_b - lo_b));
+            }
         }
-        if ((hi_b & 15u) && tid == (c1 & (PB_WG - 1u)))
-        {
-            const pb_u32x4 v = stage[c1];
-            pb_store_chunk(gout + 16 * c1, v[0], v[1], v[2], v[3], (int)(16 * c1) - (int)lo_b,
-                           (int)(hi_b - lo_b));
-        }
+        if (K.fst_dbg & 2u)
+            cf1 = cf0;
         for (uint32_t c = tid; c < nsc; c += PB_WG)
         {
-            if (c >= c0 && c < c1 && !(K.fst_dbg & 2u))
+            if (c >= cf0 && c < cf1)
                 pb_st16(gout + 16 * c, stage[c]);
             stage[c] = pb_u32x4{0u, 0u, 0u, 0u};
         }

@@ -230,6 +230,28 @@ __global__ __launch_bounds__(WG) void fill_fown2(uint8_t *dst, const uint64_t *R
             st16<false>(dst + a, u32x4{b, t, 2u, 3u});
 }
 
+// Shared boundary lines: workgroup b writes [b S + d(b), (b + 1) S + d(b + 1)) in
+// windows of wb bytes from LDS (a barrier per window), d(b) = 16 * ((b * 37) % 8) * on:
+// with on = 1 every workgroup edge splits a 128-B line between two workgroups
+// (usually on two XCDs), as packed variable-length frames do.
+__global__ __launch_bounds__(256) void fill_shift(uint8_t *dst, uint32_t S, uint32_t wb, uint32_t on)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint64_t r0 = (uint64_t)b * S + 16u * (((b * 37u) % 8u) * on);
+    const uint64_t r1 = (uint64_t)(b + 1) * S + 16u * ((((b + 1) * 37u) % 8u) * on);
+    for (uint64_t w0 = r0; w0 < r1; w0 += wb)
+    {
+        const uint32_t nc = (uint32_t)((r1 - w0 < wb ? r1 - w0 : wb) >> 4);
+        for (uint32_t q = t; q < nc; q += 256)
+            reinterpret_cast<u32x4 *>(lds)[q] = u32x4{b, q, 2u, 3u};
+        __syncthreads();
+        for (uint32_t q = t; q < nc; q += 256)
+            st16<false>(dst + w0 + 16ull * q, reinterpret_cast<const u32x4 *>(lds)[q]);
+        __syncthreads();
+    }
+}
+
 // Strided page ownership: workgroup b writes `ppw` 4 KiB pages at a stride of S
 // pages, page = ((b / S) * ppw + i) * S + b % S (S = 1: linear 4*ppw KiB; S = 8:
 // the XCD-owned layout).  Separates "8 XCDs own 8 residues" from "concurrent
@@ -477,6 +499,18 @@ int main(int argc, char **argv)
                     rep(nm, bytes, timeit([&] { hipLaunchKernelGGL(fill_fown2<1024>, dim3(nblk), dim3(1024), 0, 0, buf, dR, bs, mode, nblk); }, 20));
                 }
                 CK(hipFree(dR));
+            }
+    }
+    if (want(argc, argv, "shift"))
+    {
+        for (uint32_t S : {114688u, 24576u})
+            for (uint32_t on : {0u, 1u, 0u, 1u})
+            {
+                const uint32_t grid = (uint32_t)((g_bytes - 4096) / S / 8 * 8);
+                char nm[96];
+                snprintf(nm, sizeof nm, "shift region=%u window=16384 split-lines=%u", S, on);
+                rep(nm, (uint64_t)grid * S,
+                    timeit([&] { hipLaunchKernelGGL(fill_shift, dim3(grid), dim3(256), 29288, 0, buf, S, 16384u, on); }, 20));
             }
     }
     if (want(argc, argv, "stride"))

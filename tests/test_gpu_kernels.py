@@ -44,10 +44,10 @@ SHAPES = [
     # pb_vstage_kernel's lane layouts by window: fixed 8-lane groups (bit 4) and
     # no 32-lane groups (bit 5) build the same bytes as the default 32/16/8 layout
     ("vstage_fixed8", {"PBGPU_FST_DBG": "16"},
-     ("pb_vstage_kernel<8", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
+     ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
     ("vstage_no32", {"PBGPU_FST_DBG": "32"},
-     ("pb_vstage_kernel<8", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
+     ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
 ]
 
