@@ -285,6 +285,9 @@ def main():
             ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
             extra["d2h_umem_64B"] = d2h_rate(ctx, 0, a.packets)
             extra["d2h_umem_1500B"] = d2h_rate(ctx, 1, a.packets)
+    if not a.no_variants and a.config != "c2_udp_64" and a.config != "c5_mix" and rank == 0:
+        # the configured sequence (still loaded at index 0) landed into UMEM slots
+        extra["d2h_umem"] = d2h_rate(ctx, 0, a.packets)
     ctx.close()
     if rank != 0:
         return

@@ -23,14 +23,24 @@ for d in sorted(glob.glob(os.path.join(out_dir, "pmc_*"))):
         agg = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"]
-            if not (kn.startswith("void pb_") and ("gpf" in kn or "stage" in kn or "small" in kn or "xpage" in kn or "build_kernel" in kn)):
+            build = kn.startswith("void pb_") and ("gpf" in kn or "stage" in kn or "small" in kn or "xpage" in kn)
+            aux = kn.startswith("void pb_len_") or kn.startswith("pb_len_") or "pb_scan_blocks" in kn
+            if not (build or aux):
                 continue
-            agg[(kn, r["Counter_Name"])].append(float(r["Counter_Value"]))
-        for (kn, cn), v in agg.items():
-            e = res["per_launch"].setdefault(cfg, {"kernel": kn})
-            e[cn] = sum(v) / len(v)
+            agg[(kn, r["Counter_Name"], aux)].append(float(r["Counter_Value"]))
+        for (kn, cn, aux), v in agg.items():
+            e = res["per_launch"].setdefault(cfg, {"kernel": None, "aux": {}})
+            if aux:  # the length scan of variable-length frames: part of each step's traffic
+                e["aux"].setdefault(kn, {})[cn] = sum(v) / len(v)
+            else:
+                e["kernel"] = kn
+                e[cn] = sum(v) / len(v)
 for cfg, e in res["per_launch"].items():
     if "WRITE_SIZE" in e:
-        res["per_launch_hbm_bytes"][cfg] = int(e["WRITE_SIZE"] * 1024 + 2 * e.get("FETCH_SIZE", 0) * 1024)
+        hb = e["WRITE_SIZE"] * 1024 + 2 * e.get("FETCH_SIZE", 0) * 1024
+        for a in e["aux"].values():
+            hb += a.get("WRITE_SIZE", 0) * 1024 + 2 * a.get("FETCH_SIZE", 0) * 1024
+        res["per_launch_hbm_bytes"][cfg] = int(hb)
+        res.setdefault("packets_per_launch", {})[cfg] = 33554432
 json.dump(res, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
 print(json.dumps(res["per_launch_hbm_bytes"], indent=1))

@@ -22,8 +22,11 @@ steps = int(sys.argv[3]) if len(sys.argv) > 3 else 100
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 first_fill = next((i for i, r in enumerate(rows) if "pb_fill_kernel" in r["Kernel_Name"]), None)
 if first_fill is not None and out:
-    # the frame-build launches (the busiest kernel's shape) before the probe, runtime copies skipped
-    k, grid = out[0]["kernel"], out[0]["grid_threads"]
+    # the frame-build launches (the busiest kernel shape before the probe), runtime copies skipped
+    pre = collections.Counter()
+    for r in rows[:first_fill]:
+        pre[(r["Kernel_Name"], int(r["Grid_Size_X"]))] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    k, grid = pre.most_common(1)[0][0]
     win = [r for r in rows[:first_fill] if r["Kernel_Name"] == k and int(r["Grid_Size_X"]) == grid][-steps:]
     if len(win) == steps:
         d = sorted(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win)
