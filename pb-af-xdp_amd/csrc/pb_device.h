@@ -135,7 +135,8 @@ struct pb_kargs
 // sum, build order per frame, window list
 // (arrays for wgf own frames + PB_VST_GHOSTS earlier frames sharing the first 128-B line)
 #define PB_VST_GHOSTS 4
-#define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + ((size_t)(wgf) + PB_VST_GHOSTS) * (16 + 5) * 4 + ((size_t)(wgf) + PB_VST_GHOSTS + 2) * 4)
+#define PB_VST_PRO 208 // pb_vstage_kernel prologue records: 16 jump entries, 8 slot starts, 4 wave sums (16-B multiple)
+#define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + PB_VST_PRO + ((size_t)(wgf) + PB_VST_GHOSTS) * (16 + 5) * 4 + ((size_t)(wgf) + PB_VST_GHOSTS + 2) * 4)
 
 __device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)
 {

@@ -250,6 +250,7 @@ __device__ __forceinline__ uint32_t pb_header(const pb_kargs &K, uint32_t r0, ui
 constexpr uint32_t PB_A3 = PB_LCG_A * PB_LCG_A * PB_LCG_A;
 constexpr uint32_t PB_C3 = PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u);
 
+
 // ---------------- small fixed-length frames: one lane per frame ----------------
 //
 // Frames of <= 4*NDW bytes (configs[1] 64-B UDP, configs[3] 60-B TCP SYN, the
@@ -1431,7 +1432,10 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     const uint32_t CAP = WF + PB_VST_GHOSTS; // frames of the workgroup's arrays: ghosts + own
     pb_u32x4 *const stage = reinterpret_cast<pb_u32x4 *>(s_dyn);
     uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_dyn + (SB >> 2)); // lcg48[0 .. PB_STAGE_L48)
-    uint32_t *const s_img = s_dyn + (SB >> 2) + 2 * PB_STAGE_L48;      // header image, 16 dwords per frame
+    uint2 *const s_jt = s_l48 + PB_STAGE_L48;                          // jump[PB_JNEG - (i + hl)], i < 16
+    uint64_t *const s_st0 = reinterpret_cast<uint64_t *>(s_jt + 16);   // starts of slots 0 .. PB_VST_GHOSTS
+    uint32_t *const s_wsum = reinterpret_cast<uint32_t *>(s_st0 + 8);  // per-wave length sums
+    uint32_t *const s_img = s_dyn + (SB >> 2) + 2 * PB_STAGE_L48 + PB_VST_PRO / 4; // header image, 16 dwords per frame
     uint32_t *const s_r = s_img + CAP * 16;                            // frame start, workgroup-relative
     uint32_t *const s_len = s_r + CAP;
     uint32_t *const s_z = s_len + CAP;  // LCG state at the frame's first 16-B chunk
@@ -1453,32 +1457,24 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     const uint64_t f0 = (uint64_t)blockIdx.x * WF;
     const uint64_t left = K.n_frames - f0;
     const uint32_t nown = left < WF ? (uint32_t)left : WF;
-    const uint64_t S0 = K.fixed_len ? f0 * K.fixed_len : K.offsets[f0];
+    const uint64_t fe = f0 + nown;
     // (PBGPU_FST_DBG bit 6, A/B only: the round-1 edges at the frame starts, lines split)
     const uint64_t emask = (K.fst_dbg & 64u) ? ~0ull : ~127ull;
-    const uint64_t lo_abs = blockIdx.x ? (S0 & emask) : 0ull;
-    const uint64_t fe = f0 + nown;
-    const uint64_t hi_abs = fe < K.n_frames ? ((K.fixed_len ? fe * K.fixed_len : K.offsets[fe]) & emask)
-                                            : (K.fixed_len ? K.n_frames * K.fixed_len : K.offsets[K.n_frames]);
-    uint32_t ng = 0;
-    {
-        // ghost t = frame f0 - 1 - t, present while it ends (= frame f0 - t starts) past lo;
-        // lanes 0..3 of every wave test t = lane, the set bits are a prefix
-        const uint32_t l = tid & 63u;
-        bool g = false;
-        if (blockIdx.x && l < PB_VST_GHOSTS && f0 > l)
-            g = (K.fixed_len ? (f0 - l) * K.fixed_len : K.offsets[f0 - l]) > lo_abs;
-        const uint64_t m = __ballot(g);
-        ng = (uint32_t)__builtin_ctzll(~m);
-    }
-    const uint64_t fg = f0 - ng;   // the workgroup's first frame (a ghost if ng > 0)
-    const uint32_t nfr = ng + nown; // frames built
-    const uint64_t W0 = K.fixed_len ? fg * K.fixed_len : K.offsets[fg];
-    const uint64_t wbase = W0 & ~15ull;
-    const uint32_t lo_rel = (uint32_t)(lo_abs - wbase), hi_rel = (uint32_t)(hi_abs - wbase);
     const uint32_t nsc = SB >> 4; // stage chunks
 
-    // ---------------- A: one lane per frame; the stage starts zero ----------------
+    // ---------------- A: one lane per slot; the stage starts zero ----------------
+    // Slot j holds frame f0 - PB_VST_GHOSTS + j: the possible ghosts, then the own
+    // frames.  The lengths come from the seeds and the starts from a workgroup scan
+    // of them on top of one offset, so the global loads (that offset, the jump
+    // entries, lcg48) are independent of each other and their latency overlaps the
+    // seed / header arithmetic (a chain offsets -> ghosts -> offsets -> jump entry
+    // was ~3 dependent load round trips per workgroup).
+    constexpr uint32_t GH = PB_VST_GHOSTS;
+    const int64_t fb = (int64_t)f0 - (int64_t)GH;
+    const uint64_t base0 = fb <= 0 ? 0ull : (K.fixed_len ? (uint64_t)fb * K.fixed_len : K.offsets[fb]);
+    uint2 jtv = make_uint2(0u, 0u);
+    if (tid < 16u) // state at payload index -((r % 16) + hl): the first byte of the frame's first chunk
+        jtv = K.jump[PB_JNEG - (tid + hl)];
     uint2 l48v[(PB_STAGE_L48 + PB_WG - 1) / PB_WG];
 #pragma unroll
     for (uint32_t i = 0; i < (PB_STAGE_L48 + PB_WG - 1) / PB_WG; ++i)
@@ -1486,56 +1482,98 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             l48v[i] = K.lcg48[tid + i * PB_WG];
     for (uint32_t c = tid; c < nsc; c += PB_WG)
         stage[c] = pb_u32x4{0u, 0u, 0u, 0u};
-    uint32_t my_r = 0;
     const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
-    if (tid < nfr)
+    const int64_t fj = fb + (int64_t)tid;
+    const bool valid = tid < CAP && fj >= 0 && (uint64_t)fj < fe;
+    uint32_t flen = 0, st0 = 0, hsf = 0;
+    uint32_t d[16];
+    if (valid)
     {
-        const uint64_t f = fg + tid;
-        uint64_t base;
-        uint32_t flen;
-        if (K.fixed_len)
-        {
-            base = f * K.fixed_len;
-            flen = K.fixed_len;
-        }
-        else
-        {
-            base = K.offsets[f];
-            flen = (uint32_t)(K.offsets[f + 1] - base);
-        }
-        my_r = (uint32_t)(base - wbase);
-        // state at payload index -((r % 16) + hl): the first byte of the frame's first chunk
-        const uint2 jt = K.jump[PB_JNEG - ((my_r & 15u) + hl)];
         uint64_t k;
         uint32_t pi;
-        pb_frame_index(K, f, k, pi);
+        pb_frame_index(K, (uint64_t)fj, k, pi);
         const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
         const uint32_t r0 = pb_rand_r(s);
         const pb_frame_pl P = pb_payload(K, s, pi);
-        uint32_t d[16];
         const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
-        pb_u32x4 *row = reinterpret_cast<pb_u32x4 *>(s_img + tid * 16);
-        row[0] = pb_u32x4{d[0], d[1], d[2], d[3]};
-        row[1] = pb_u32x4{d[4], d[5], d[6], d[7]};
-        row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
-        row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
-        s_r[tid] = my_r;
-        s_len[tid] = flen;
-        s_z[tid] = jt.x * P.st0 + jt.y;
+        flen = K.fixed_len ? K.fixed_len : hl + P.plen;
+        st0 = P.st0;
         if (L4)
         {
             uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) +
                           pb_halves(d[12]) + pb_halves(d[13]);
             if (flags & PBK_PSEUDO)
                 hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
-            s_hs[tid] = pb_fold(hs);
+            hsf = pb_fold(hs);
         }
     }
+    // frame starts: exclusive scan of the slot lengths (in-wave shuffles, wave totals via LDS)
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    uint32_t inc = flen;
+#pragma unroll
+    for (uint32_t dd = 1; dd < 64; dd <<= 1)
+    {
+        const uint32_t y = __shfl_up(inc, dd, 64);
+        inc += lane >= dd ? y : 0u;
+    }
+    if (lane == 63u)
+        s_wsum[wv] = inc;
+    if (tid <= GH) // slots 0 .. GH are in wave 0: no earlier waves
+        s_st0[tid] = base0 + (inc - flen);
+    if (tid < 16u)
+        s_jt[tid] = jtv;
 #pragma unroll
     for (uint32_t i = 0; i < (PB_STAGE_L48 + PB_WG - 1) / PB_WG; ++i)
         if (tid + i * PB_WG < PB_STAGE_L48)
             s_l48[tid + i * PB_WG] = l48v[i];
     __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < PB_WG / 64; ++w)
+    {
+        const uint32_t t = s_wsum[w];
+        pre += w < wv ? t : 0u;
+        tot += t;
+    }
+    const uint64_t start = base0 + pre + (inc - flen);
+    // Workgroup b owns frames [f0, f0 + nown) and stores exactly the output bytes
+    // [lo, hi): lo = the 128-B line holding its first frame's start (0 for b = 0), hi =
+    // the next workgroup's lo.  No line is written by two workgroups (two XCDs): an
+    // edge that split a line cost 5-12% of the write rate (profiles/r02/wbench,
+    // shift_*.txt).  The bytes of [lo, start(f0)) belong to up to PB_VST_GHOSTS earlier
+    // frames ("ghosts"), built here in full (their checksums need every byte) and
+    // stored only inside [lo, hi); the bytes of the own last frames past hi are the
+    // next workgroup's ghosts.
+    const uint64_t S0 = s_st0[GH];
+    const uint64_t lo_abs = blockIdx.x ? (S0 & emask) : 0ull;
+    const uint64_t hi_abs = fe < K.n_frames ? ((base0 + tot) & emask) : base0 + tot;
+    uint32_t ng = 0;
+    // ghost l = frame f0 - 1 - l, present while it ends (= frame f0 - l starts) past lo;
+    // the ghosts are a prefix l = 0, 1, ...
+    if (blockIdx.x)
+        while (ng < GH && f0 > ng && s_st0[GH - ng] > lo_abs)
+            ++ng;
+    const uint32_t nfr = ng + nown; // frames built: ghosts + own, array index t = slot - (GH - ng)
+    const uint64_t wbase = s_st0[GH - ng] & ~15ull;
+    const uint32_t lo_rel = (uint32_t)(lo_abs - wbase), hi_rel = (uint32_t)(hi_abs - wbase);
+    const int32_t tix = (int32_t)tid - (int32_t)(GH - ng);
+    if (valid && tix >= 0)
+    {
+        const uint32_t r = (uint32_t)(start - wbase);
+        const uint2 jt = s_jt[r & 15u];
+        pb_u32x4 *row = reinterpret_cast<pb_u32x4 *>(s_img + tix * 16);
+        row[0] = pb_u32x4{d[0], d[1], d[2], d[3]};
+        row[1] = pb_u32x4{d[4], d[5], d[6], d[7]};
+        row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
+        row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
+        s_r[tix] = r;
+        s_len[tix] = flen;
+        s_z[tix] = jt.x * st0 + jt.y;
+        if (L4)
+            s_hs[tix] = hsf;
+    }
+    __syncthreads();
+    const uint32_t my_r = tid < nfr ? s_r[tid] : 0u;
     // window starts: frame t opens windows (r_{t-1} / W, r_t / W]  (W >= the longest frame)
     if (tid < nfr)
     {
@@ -1761,6 +1799,8 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         }
         if (K.fst_dbg & 2u)
             cf1 = cf0;
+        // (one chunk per step: four LDS reads in flight, then four stores, measured 1.7%
+        // slower on configs[2])
         for (uint32_t c = tid; c < nsc; c += PB_WG)
         {
             if (c >= cf0 && c < cf1)

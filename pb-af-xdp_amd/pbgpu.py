@@ -248,14 +248,14 @@ def parse_mac(s: Optional[str]) -> bytes:
 
 
 # --------------------------------------------------------------- library
-_lib = None
+_libs = {}
 
 
 def load_library(path: str = LIB_PATH) -> C.CDLL:
-    """Load libpbgpu.so (raises if it is absent: there is no CPU fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
+    """Load libpbgpu.so (raises if it is absent: there is no CPU fallback).
+    Other paths load other builds side by side (compile-time A/B probes)."""
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise FileNotFoundError(f"{path} not built (run `make -C pb-af-xdp_amd`): the GPU path has no fallback")
     lib = C.CDLL(path)
@@ -293,7 +293,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
