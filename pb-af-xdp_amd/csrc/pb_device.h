@@ -128,6 +128,12 @@ struct pb_kargs
                             // pb_vstage_kernel: bit 4 fixed 8-lane groups, bit 5 no 32-lane groups (A/B)
     uint32_t lds_pad;       // dynamic LDS added to the build launch: caps workgroups per CU (fewer
                             // concurrent writers)
+    // pb_vstage_kernel, variable length: per-workgroup length sums (stage_wgf frames each) and
+    // their exclusive scan per 256 workgroups (pb_len_wgsum + pb_scan_blocks); the kernel then
+    // writes offsets_w for its own frames.  Null: offsets[] was scanned beforehand (3 passes).
+    const uint32_t *vblk_sum;
+    const unsigned long long *vblk_l2;
+    uint64_t *offsets_w;
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)
@@ -135,7 +141,7 @@ struct pb_kargs
 // sum, build order per frame, window list
 // (arrays for wgf own frames + PB_VST_GHOSTS earlier frames sharing the first 128-B line)
 #define PB_VST_GHOSTS 4
-#define PB_VST_PRO 208 // pb_vstage_kernel prologue records: 16 jump entries, 8 slot starts, 4 wave sums (16-B multiple)
+#define PB_VST_PRO 240 // pb_vstage_kernel prologue records: 16 jump entries, 12 starts / S0 parts, 4 wave sums (16-B multiple)
 #define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + PB_VST_PRO + ((size_t)(wgf) + PB_VST_GHOSTS) * (16 + 5) * 4 + ((size_t)(wgf) + PB_VST_GHOSTS + 2) * 4)
 
 __device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)

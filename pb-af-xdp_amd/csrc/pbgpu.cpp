@@ -25,6 +25,8 @@
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st);
 extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
                                          uint64_t *offsets, hipStream_t st);
+extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t *bsum, uint32_t nblk, unsigned long long *l2,
+                                             uint32_t n_l2, uint64_t *offsets, hipStream_t st);
 extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *offsets, uint64_t first, uint32_t n,
                                          uint8_t *dst, uint32_t stride, uint16_t *lens, hipStream_t st);
 extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipStream_t st);
@@ -34,6 +36,21 @@ extern "C" hipError_t pbk_launch_scatter_fixed(const uint8_t *src, uint32_t flen
 
 #define PB_JUMP_N (65536 + 256) // entries j = -PB_JNEG .. 65536 + 175
 #define PB_SCAN_FRAMES_PER_BLOCK (256 * 8)
+#define PB_VST_SCAN_MIN_WGF 32 // smallest pb_vstage_kernel workgroup the scratch is sized for
+
+// device scratch of a frames buffer: the 3-pass length scan's block sums, or pb_vstage_kernel's
+// per-workgroup length sums (u32) + their per-256 group sums (u64)
+static uint64_t vst_bsum_bytes(uint64_t nblk)
+{
+    return (nblk * 4 + 15) & ~15ull;
+}
+static uint64_t scan_tmp_bytes(uint64_t capacity_frames)
+{
+    const uint64_t a = (capacity_frames / PB_SCAN_FRAMES_PER_BLOCK + 1) * 8;
+    const uint64_t nblk = capacity_frames / PB_VST_SCAN_MIN_WGF + 1;
+    const uint64_t b = vst_bsum_bytes(nblk) + (nblk / 256 + 1) * 8;
+    return a > b ? a : b;
+}
 
 namespace
 {
@@ -946,11 +963,10 @@ int pbgpu_frames_alloc(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capaci
     if (f == NULL)
         return PBGPU_ENOMEM;
     capacity_bytes = (capacity_bytes + 15) & ~15ull;
-    const uint64_t nblocks = capacity_frames / PB_SCAN_FRAMES_PER_BLOCK + 1;
     // +64 B: word-granular readers (UMEM scatter) may touch a few bytes past the last frame
     if (hipMalloc((void **)&f->data, capacity_bytes + 64) != hipSuccess ||
         hipMalloc((void **)&f->offsets, (capacity_frames + 1) * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc((void **)&f->scan_tmp, nblocks * sizeof(uint64_t)) != hipSuccess)
+        hipMalloc((void **)&f->scan_tmp, scan_tmp_bytes(capacity_frames)) != hipSuccess)
     {
         pbgpu_frames_free(ctx, f);
         return PBGPU_ENOMEM;
@@ -1087,9 +1103,28 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     else
     {
         out->total_bytes = UINT64_MAX;
-        const uint64_t nblocks = (nf + PB_SCAN_FRAMES_PER_BLOCK - 1) / PB_SCAN_FRAMES_PER_BLOCK;
-        HIPCHK(pbk_launch_lengths(&K, (unsigned long long *)out->scan_tmp, (uint32_t)nblocks, out->offsets,
-                                  ctx->stream));
+        K.vblk_sum = nullptr;
+        K.vblk_l2 = nullptr;
+        K.offsets_w = nullptr;
+        if (K.vst && K.stage_wgf >= PB_VST_SCAN_MIN_WGF && !env_is("PBGPU_VST_SCAN", "3pass"))
+        {
+            // pb_vstage_kernel: per-workgroup length sums, their scan, offsets written by the build
+            const uint64_t nblk = (nf + K.stage_wgf - 1) / K.stage_wgf;
+            const uint64_t n_l2 = (nblk + 255) / 256;
+            uint32_t *bsum = reinterpret_cast<uint32_t *>(out->scan_tmp);
+            unsigned long long *l2 =
+                reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(out->scan_tmp) + vst_bsum_bytes(nblk));
+            HIPCHK(pbk_launch_vst_lengths(&K, bsum, (uint32_t)nblk, l2, (uint32_t)n_l2, out->offsets, ctx->stream));
+            K.vblk_sum = bsum;
+            K.vblk_l2 = l2;
+            K.offsets_w = out->offsets;
+        }
+        else
+        {
+            const uint64_t nblocks = (nf + PB_SCAN_FRAMES_PER_BLOCK - 1) / PB_SCAN_FRAMES_PER_BLOCK;
+            HIPCHK(pbk_launch_lengths(&K, (unsigned long long *)out->scan_tmp, (uint32_t)nblocks, out->offsets,
+                                      ctx->stream));
+        }
     }
     K.xs_grid = 0;
     if (K.small_ndw && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && !env_is("PBGPU_KERNEL", "linear"))

@@ -1433,8 +1433,8 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     pb_u32x4 *const stage = reinterpret_cast<pb_u32x4 *>(s_dyn);
     uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_dyn + (SB >> 2)); // lcg48[0 .. PB_STAGE_L48)
     uint2 *const s_jt = s_l48 + PB_STAGE_L48;                          // jump[PB_JNEG - (i + hl)], i < 16
-    uint64_t *const s_st0 = reinterpret_cast<uint64_t *>(s_jt + 16);   // starts of slots 0 .. PB_VST_GHOSTS
-    uint32_t *const s_wsum = reinterpret_cast<uint32_t *>(s_st0 + 8);  // per-wave length sums
+    uint64_t *const s_st0 = reinterpret_cast<uint64_t *>(s_jt + 16);   // [0, GH]: slot starts - base0; [8, 12): S0 parts
+    uint32_t *const s_wsum = reinterpret_cast<uint32_t *>(s_st0 + 12); // per-wave length sums
     uint32_t *const s_img = s_dyn + (SB >> 2) + 2 * PB_STAGE_L48 + PB_VST_PRO / 4; // header image, 16 dwords per frame
     uint32_t *const s_r = s_img + CAP * 16;                            // frame start, workgroup-relative
     uint32_t *const s_len = s_r + CAP;
@@ -1471,7 +1471,14 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     // was ~3 dependent load round trips per workgroup).
     constexpr uint32_t GH = PB_VST_GHOSTS;
     const int64_t fb = (int64_t)f0 - (int64_t)GH;
-    const uint64_t base0 = fb <= 0 ? 0ull : (K.fixed_len ? (uint64_t)fb * K.fixed_len : K.offsets[fb]);
+    // start of frame f0: fixed length, or the scanned per-workgroup length sums (l2 prefix of
+    // this workgroup's group of 256 + the sums of the earlier workgroups of the group), or
+    // offsets[] when the 3-pass scan ran
+    const bool bsum = !K.fixed_len && K.vblk_sum != nullptr;
+    uint64_t s0_part = 0;
+    if (bsum && tid < (blockIdx.x & 255u))
+        s0_part = K.vblk_sum[(blockIdx.x & ~255u) + tid];
+    const uint64_t s0_base = K.fixed_len ? f0 * K.fixed_len : (bsum ? K.vblk_l2[blockIdx.x >> 8] : K.offsets[f0]);
     uint2 jtv = make_uint2(0u, 0u);
     if (tid < 16u) // state at payload index -((r % 16) + hl): the first byte of the frame's first chunk
         jtv = K.jump[PB_JNEG - (tid + hl)];
@@ -1516,10 +1523,15 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         const uint32_t y = __shfl_up(inc, dd, 64);
         inc += lane >= dd ? y : 0u;
     }
+#pragma unroll
+    for (uint32_t dd = 32; dd > 0; dd >>= 1)
+        s0_part += __shfl_xor(s0_part, dd, 64);
     if (lane == 63u)
         s_wsum[wv] = inc;
+    if (lane == 0u)
+        s_st0[8 + wv] = s0_part;
     if (tid <= GH) // slots 0 .. GH are in wave 0: no earlier waves
-        s_st0[tid] = base0 + (inc - flen);
+        s_st0[tid] = inc - flen;
     if (tid < 16u)
         s_jt[tid] = jtv;
 #pragma unroll
@@ -1535,7 +1547,14 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         pre += w < wv ? t : 0u;
         tot += t;
     }
+    uint64_t S0 = s0_base;
+#pragma unroll
+    for (uint32_t w = 0; w < PB_WG / 64; ++w)
+        S0 += s_st0[8 + w];
+    const uint64_t base0 = S0 - s_st0[GH]; // start of slot 0 (the valid ghost slots' lengths before f0)
     const uint64_t start = base0 + pre + (inc - flen);
+    if (bsum && valid && tid >= GH) // own frames: the offsets the 3-pass scan would have written
+        K.offsets_w[(uint64_t)fj] = start;
     // Workgroup b owns frames [f0, f0 + nown) and stores exactly the output bytes
     // [lo, hi): lo = the 128-B line holding its first frame's start (0 for b = 0), hi =
     // the next workgroup's lo.  No line is written by two workgroups (two XCDs): an
@@ -1544,17 +1563,16 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     // frames ("ghosts"), built here in full (their checksums need every byte) and
     // stored only inside [lo, hi); the bytes of the own last frames past hi are the
     // next workgroup's ghosts.
-    const uint64_t S0 = s_st0[GH];
     const uint64_t lo_abs = blockIdx.x ? (S0 & emask) : 0ull;
     const uint64_t hi_abs = fe < K.n_frames ? ((base0 + tot) & emask) : base0 + tot;
     uint32_t ng = 0;
     // ghost l = frame f0 - 1 - l, present while it ends (= frame f0 - l starts) past lo;
     // the ghosts are a prefix l = 0, 1, ...
     if (blockIdx.x)
-        while (ng < GH && f0 > ng && s_st0[GH - ng] > lo_abs)
+        while (ng < GH && f0 > ng && base0 + s_st0[GH - ng] > lo_abs)
             ++ng;
     const uint32_t nfr = ng + nown; // frames built: ghosts + own, array index t = slot - (GH - ng)
-    const uint64_t wbase = s_st0[GH - ng] & ~15ull;
+    const uint64_t wbase = (base0 + s_st0[GH - ng]) & ~15ull;
     const uint32_t lo_rel = (uint32_t)(lo_abs - wbase), hi_rel = (uint32_t)(hi_abs - wbase);
     const int32_t tix = (int32_t)tid - (int32_t)(GH - ng);
     if (valid && tix >= 0)
@@ -2150,6 +2168,43 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
     }
     else
         return hipErrorInvalidValue; // pbgpu_load_sequence selects one of the kernels above for every sequence
+    return hipGetLastError();
+}
+
+// pb_vstage_kernel's length pass: lane b sums the lengths of workgroup b's wgf frames
+// (bsum[b]), each 256-lane group the sums of its 256 workgroups (l2[group], scanned next
+// by pb_scan_blocks); the build kernel writes offsets[] itself
+__global__ __launch_bounds__(256) void pb_len_wgsum(pb_kargs K, uint32_t wgf, uint32_t nblk, uint32_t *bsum,
+                                                    unsigned long long *l2)
+{
+    __shared__ unsigned long long s_w[4];
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    uint32_t sum = 0;
+    if (b < nblk)
+    {
+        const uint64_t fa = (uint64_t)b * wgf;
+        const uint64_t fz = fa + wgf < K.n_frames ? fa + wgf : K.n_frames;
+#pragma unroll 4
+        for (uint64_t f = fa; f < fz; ++f)
+            sum += pb_frame_len(K, f);
+        bsum[b] = sum;
+    }
+    unsigned long long v = sum;
+#pragma unroll
+    for (uint32_t dd = 32; dd > 0; dd >>= 1)
+        v += __shfl_xor(v, dd, 64);
+    if ((threadIdx.x & 63u) == 0)
+        s_w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        l2[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t *bsum, uint32_t nblk, unsigned long long *l2,
+                                             uint32_t n_l2, uint64_t *offsets, hipStream_t st)
+{
+    hipLaunchKernelGGL(pb_len_wgsum, dim3(n_l2), dim3(256), 0, st, *K, K->stage_wgf, nblk, bsum, l2);
+    hipLaunchKernelGGL(pb_scan_blocks, dim3(1), dim3(1024), 0, st, l2, n_l2, offsets, K->n_frames, K->counters);
     return hipGetLastError();
 }
 
