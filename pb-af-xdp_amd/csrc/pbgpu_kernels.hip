@@ -373,6 +373,34 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
             if ((uint32_t)(4 * t) < flen)
                 s_tile[w0 + t] = d[t];
     }
+    else if ((flen & 3u) == 2u)
+    {
+        // 2 mod 4 (98-B ICMP, 106-B UDP): frames start on even bytes, so a frame is one 16-bit
+        // half dword at one end and nw = (flen - 2) / 4 whole dwords, written two per
+        // ds_write2_b32 (4-B alignment is all a pair needs) instead of dword + byte writes
+        const uint32_t nw = (flen - 2u) >> 2;
+        const bool odd = (B & 2u) != 0; // starts at byte 2 of a dword: the half dword comes first
+        uint16_t *const half = reinterpret_cast<uint16_t *>(s_tile) + ((odd ? B : B + flen - 2u) >> 1);
+        *half = (uint16_t)(odd ? d[0] : (d[nw] & 0xFFFFu));
+        uint32_t *const row = s_tile + ((B + (odd ? 2u : 0u)) >> 2);
+#pragma unroll
+        for (int u = 0; u < NDW; u += 2)
+        {
+            if ((uint32_t)u < nw)
+            {
+                const uint32_t v0 = odd ? __builtin_amdgcn_alignbyte(d[u + 1], d[u], 2u) : d[u];
+                if ((uint32_t)u + 1u < nw)
+                {
+                    const uint32_t v1 =
+                        odd ? __builtin_amdgcn_alignbyte(u + 2 < NDW ? d[u + 2] : 0u, d[u + 1], 2u) : d[u + 1];
+                    const uint2 pr = make_uint2(v0, v1);
+                    __builtin_memcpy(row + u, &pr, 8);
+                }
+                else
+                    row[u] = v0;
+            }
+        }
+    }
     else
     {
         // frame starts at byte phase sh of a dword: out dword u = frame bytes [4u - sh, 4u - sh + 4)
