@@ -841,10 +841,10 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             }
             else
             {
-                // 24 KiB windows for pb_stage_kernel, 16 for pb_vstage_kernel (configs[2], 2^23
-                // frames: 1.74 ms at 16 KiB, 1.86 at 24, 2.40 at 36, 2.46 at 8; profiles/r01/vstage)
-                const bool vst_ok = K.gpf_rmode == 1 && !(flags & PBK_LITERAL) && !env_is("PBGPU_KERNEL", "stage");
-                const uint32_t skb = ekb && atoi(ekb) > 0 ? (uint32_t)atoi(ekb) : (vst_ok ? 16 : 24);
+                // 24 KiB windows.  pb_vstage_kernel (configs[2], 2^25 frames, profiles/r02/ab/hv2_*):
+                // 6.37 ms at 24 KiB, 6.68 at 16, 7.34 at 28 (3 workgroups per CU) since it keeps
+                // only 9 header dwords per frame in LDS; with 16-dword images 16 KiB was best
+                const uint32_t skb = ekb && atoi(ekb) > 0 ? (uint32_t)atoi(ekb) : 24;
                 sbytes = (skb * 1024 + 15) / 16 * 16;
                 if (sbytes < 2 * maxf + 48)
                     sbytes = (2 * maxf + 48 + 15) / 16 * 16;

@@ -1463,8 +1463,11 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     uint2 *const s_jt = s_l48 + PB_STAGE_L48;                          // jump[PB_JNEG - (i + hl)], i < 16
     uint64_t *const s_st0 = reinterpret_cast<uint64_t *>(s_jt + 16);   // [0, GH]: slot starts - base0; [8, 12): S0 parts
     uint32_t *const s_wsum = reinterpret_cast<uint32_t *>(s_st0 + 12); // per-wave length sums
-    uint32_t *const s_img = s_dyn + (SB >> 2) + 2 * PB_STAGE_L48 + PB_VST_PRO / 4; // header image, 16 dwords per frame
-    uint32_t *const s_r = s_img + CAP * 16;                            // frame start, workgroup-relative
+    uint32_t *const s_tm = s_wsum + 4;                                 // the header template (16 dwords)
+    // per frame only header dwords [PB_VST_HV0, PB_VST_HV0 + PB_VST_HVN) (every per-frame field and
+    // the checksums); the others are the template's
+    uint32_t *const s_hv = s_dyn + (SB >> 2) + 2 * PB_STAGE_L48 + PB_VST_PRO / 4;
+    uint32_t *const s_r = s_hv + CAP * PB_VST_HVN;                     // frame start, workgroup-relative
     uint32_t *const s_len = s_r + CAP;
     uint32_t *const s_z = s_len + CAP;  // LCG state at the frame's first 16-B chunk
     uint32_t *const s_hs = s_z + CAP;   // header + pseudo header word sum, folded (frame alignment)
@@ -1562,6 +1565,14 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         s_st0[tid] = inc - flen;
     if (tid < 16u)
         s_jt[tid] = jtv;
+    if (tid == 0u)
+    {
+        pb_u32x4 *const tm = reinterpret_cast<pb_u32x4 *>(s_tm);
+        tm[0] = pb_u32x4{K.tmpl[0], K.tmpl[1], K.tmpl[2], K.tmpl[3]};
+        tm[1] = pb_u32x4{K.tmpl[4], K.tmpl[5], K.tmpl[6], K.tmpl[7]};
+        tm[2] = pb_u32x4{K.tmpl[8], K.tmpl[9], K.tmpl[10], K.tmpl[11]};
+        tm[3] = pb_u32x4{K.tmpl[12], K.tmpl[13], K.tmpl[14], K.tmpl[15]};
+    }
 #pragma unroll
     for (uint32_t i = 0; i < (PB_STAGE_L48 + PB_WG - 1) / PB_WG; ++i)
         if (tid + i * PB_WG < PB_STAGE_L48)
@@ -1607,11 +1618,10 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     {
         const uint32_t r = (uint32_t)(start - wbase);
         const uint2 jt = s_jt[r & 15u];
-        pb_u32x4 *row = reinterpret_cast<pb_u32x4 *>(s_img + tix * 16);
-        row[0] = pb_u32x4{d[0], d[1], d[2], d[3]};
-        row[1] = pb_u32x4{d[4], d[5], d[6], d[7]};
-        row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
-        row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
+        uint32_t *const hv = s_hv + tix * PB_VST_HVN;
+#pragma unroll
+        for (uint32_t w = 0; w < PB_VST_HVN; ++w)
+            hv[w] = d[PB_VST_HV0 + w];
         s_r[tix] = r;
         s_len[tix] = flen;
         s_z[tix] = jt.x * st0 + jt.y;
@@ -1756,7 +1766,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                     edge(m, p);
                 }
             }
-            uint32_t *const img = s_img + fr * 16;
+            uint32_t *const hv = s_hv + fr * PB_VST_HVN;
             if (L4)
             {
                 if (G == 8)
@@ -1776,7 +1786,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                     if (r & 1u)
                         pc = pb_bswap16(pc);
                     const uint32_t c = (~pb_fold(s_hs[fr] + pc)) & 0xFFFFu;
-                    img[K.csum_dw] |= K.csum_hi ? (c << 16) : c;
+                    hv[K.csum_dw - PB_VST_HV0] |= K.csum_hi ? (c << 16) : c;
                 }
             }
             // header chunks 0 .. nhc-1: the image shifted to byte s0 (the image is zero past hl);
@@ -1785,9 +1795,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             const uint32_t nhc = (hend + 15u) >> 4;
             if (lg < nhc)
             {
-                // frame bytes [16 lg - s0, 16 lg - s0 + 16): image dwords i0 .. i0 + 4, those
-                // outside the 16-dword row (a neighbour's image or another LDS array; never
-                // outside the allocation) read as zero
+                // frame bytes [16 lg - s0, 16 lg - s0 + 16): header dwords i0 .. i0 + 4 (the frame's
+                // own for [PB_VST_HV0, PB_VST_HV0 + PB_VST_HVN), else the template's); those outside
+                // the 16-dword header read as zero
                 const int xb = (int)(16u * lg) - (int)s0;
                 const int i0 = xb >> 2;
                 const uint32_t sh = (uint32_t)xb & 3u;
@@ -1795,8 +1805,11 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
 #pragma unroll
                 for (int t = 0; t < 5; ++t)
                 {
-                    const uint32_t v = img[i0 + t];
-                    wv[t] = (uint32_t)(i0 + t) < 16u ? v : 0u;
+                    const int ix = i0 + t;
+                    const uint32_t *src =
+                        (uint32_t)(ix - (int)PB_VST_HV0) < PB_VST_HVN ? hv + (ix - (int)PB_VST_HV0) : s_tm + (ix & 15);
+                    const uint32_t v = *src;
+                    wv[t] = (uint32_t)ix < 16u ? v : 0u;
                 }
                 uint32_t h[4];
 #pragma unroll
