@@ -872,8 +872,14 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 {
                     K.vst = 1;
                     K.fst_dbg = (uint32_t)env_int("PBGPU_FST_DBG", 0);
-                    // phase A has one lane per frame for the own frames and the ghosts
-                    K.stage_wgf = std::min<uint32_t>(K.stage_wgf, PB_WG - PB_VST_GHOSTS);
+                    // phase A has one lane per slot (ghosts + own frames): as many own frames as
+                    // lanes allow, which also spreads the per-workgroup work over the most windows
+                    // (configs[2], 2^25 frames: 6.37 ms at 240-252 vs 6.44 at 218 and 6.50 at 200;
+                    // profiles/r02/ab/wf24*)
+                    K.stage_wgf = getenv("PBGPU_WGF") || K.fixed_len ? std::min<uint32_t>(K.stage_wgf, PB_WG - PB_VST_GHOSTS)
+                                                                     : PB_WG - PB_VST_GHOSTS;
+                    if (K.stage_bytes + PB_VST_LDS(K.stage_wgf) > 64 * 1024)
+                        K.stage_wgf = wgf > PB_WG - PB_VST_GHOSTS ? PB_WG - PB_VST_GHOSTS : wgf;
                 }
             }
             // fixed-length staged kernel (pb_fstage_kernel): lengths > 128 B that are a
