@@ -141,10 +141,11 @@ struct pb_kargs
 // sum, build order per frame, window list
 // (arrays for wgf own frames + PB_VST_GHOSTS earlier frames sharing the first 128-B line)
 #define PB_VST_GHOSTS 4
-#define PB_VST_PRO 304 // pb_vstage_kernel prologue records: 16 jump entries, 12 starts / S0 parts, 4 wave sums, template (16-B multiple)
+#define PB_VST_PRO 576 // pb_vstage_kernel prologue records: 16 jump entries, 12 starts / S0 parts, 4 wave sums, template, 17 chunk masks (16-B multiple)
 #define PB_VST_HV0 4u  // per-frame header dwords kept in LDS: [4, 13) = IPv4 from tot_len to the L4 checksum
 #define PB_VST_HVN 9u  // (UDP csum dword 10, TCP 12, ICMP 9); dwords 0-3 and 13-15 are the template's
-#define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + PB_VST_PRO + ((size_t)(wgf) + PB_VST_GHOSTS) * (PB_VST_HVN + 5) * 4 + ((size_t)(wgf) + PB_VST_GHOSTS + 2) * 4)
+#define PB_VST_CAP(wgf) (((size_t)(wgf) + PB_VST_GHOSTS + 1) & ~(size_t)1)
+#define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + PB_VST_PRO + PB_VST_CAP(wgf) * (PB_VST_HVN + 5) * 4 + (PB_VST_CAP(wgf) + 2) * 4)
 
 __device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)
 {

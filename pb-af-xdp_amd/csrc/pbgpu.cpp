@@ -876,10 +876,15 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                     // lanes allow, which also spreads the per-workgroup work over the most windows
                     // (configs[2], 2^25 frames: 6.37 ms at 240-252 vs 6.44 at 218 and 6.50 at 200;
                     // profiles/r02/ab/wf24*)
-                    K.stage_wgf = getenv("PBGPU_WGF") || K.fixed_len ? std::min<uint32_t>(K.stage_wgf, PB_WG - PB_VST_GHOSTS)
-                                                                     : PB_WG - PB_VST_GHOSTS;
-                    if (K.stage_bytes + PB_VST_LDS(K.stage_wgf) > 64 * 1024)
-                        K.stage_wgf = wgf > PB_WG - PB_VST_GHOSTS ? PB_WG - PB_VST_GHOSTS : wgf;
+                    // (as many as still leave 4 workgroups per CU when the window's frames fit)
+                    K.stage_wgf = std::min<uint32_t>(K.stage_wgf, PB_WG - PB_VST_GHOSTS);
+                    if (!getenv("PBGPU_WGF") && !K.fixed_len)
+                    {
+                        uint32_t best = PB_WG - PB_VST_GHOSTS;
+                        while (best > K.stage_wgf && K.stage_bytes + PB_VST_LDS(best) > 160 * 1024 / 4)
+                            --best;
+                        K.stage_wgf = best;
+                    }
                 }
             }
             // fixed-length staged kernel (pb_fstage_kernel): lengths > 128 B that are a
@@ -1150,7 +1155,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     int rc = PBGPU_OK;
     if (!span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
         return rc;
-    const bool timing = K.stage_win && !K.fst_g && !K.vst && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
+    const bool timing = K.stage_win && !K.fst_g && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
     const uint64_t n_wg = K.stage_wgf ? (nf + K.stage_wgf - 1) / K.stage_wgf : 0;
     if (timing)
     {

@@ -1457,13 +1457,14 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     constexpr uint32_t NGW = PB_WG / G; // frames in flight per workgroup
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     const uint32_t WF = K.stage_wgf, W = K.stage_win, SB = K.stage_bytes;
-    const uint32_t CAP = WF + PB_VST_GHOSTS; // frames of the workgroup's arrays: ghosts + own
+    const uint32_t CAP = (WF + PB_VST_GHOSTS + 1u) & ~1u; // frames of the workgroup's arrays: ghosts + own (rounded to even)
     pb_u32x4 *const stage = reinterpret_cast<pb_u32x4 *>(s_dyn);
     uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_dyn + (SB >> 2)); // lcg48[0 .. PB_STAGE_L48)
     uint2 *const s_jt = s_l48 + PB_STAGE_L48;                          // jump[PB_JNEG - (i + hl)], i < 16
     uint64_t *const s_st0 = reinterpret_cast<uint64_t *>(s_jt + 16);   // [0, GH]: slot starts - base0; [8, 12): S0 parts
     uint32_t *const s_wsum = reinterpret_cast<uint32_t *>(s_st0 + 12); // per-wave length sums
     uint32_t *const s_tm = s_wsum + 4;                                 // the header template (16 dwords)
+    pb_u32x4 *const s_m16 = reinterpret_cast<pb_u32x4 *>(s_tm + 16);   // s_m16[k]: chunk bytes >= k set, k <= 16
     // per frame only header dwords [PB_VST_HV0, PB_VST_HV0 + PB_VST_HVN) (every per-frame field and
     // the checksums); the others are the template's
     uint32_t *const s_hv = s_dyn + (SB >> 2) + 2 * PB_STAGE_L48 + PB_VST_PRO / 4;
@@ -1477,6 +1478,10 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     const uint32_t tid = threadIdx.x;
     const uint32_t flags = K.flags;
     const uint32_t hl = K.hl;
+    unsigned long long tt = 0; // PB_TIMING builds: phase stamps (slot 1 A, 3 windows + order, 2 B, 4 S)
+    PB_STAMP(0);
+    if (PB_TIMING)
+        tt = __builtin_amdgcn_s_memtime();
     // Workgroup b owns frames [f0, f0 + nown) and stores exactly the output bytes
     // [lo, hi): lo = the 128-B line holding its first frame's start (0 for b = 0), hi =
     // the next workgroup's lo.  No line is written by two workgroups (two XCDs): an
@@ -1565,6 +1570,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         s_st0[tid] = inc - flen;
     if (tid < 16u)
         s_jt[tid] = jtv;
+    if (tid <= 16u)
+        s_m16[tid] = pb_u32x4{pb_range_mask((int)tid, 4), pb_range_mask((int)tid - 4, 4), pb_range_mask((int)tid - 8, 4),
+                              pb_range_mask((int)tid - 12, 4)};
     if (tid == 0u)
     {
         pb_u32x4 *const tm = reinterpret_cast<pb_u32x4 *>(s_tm);
@@ -1629,6 +1637,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             s_hs[tix] = hsf;
     }
     __syncthreads();
+    PB_LAP(1, tt);
     const uint32_t my_r = tid < nfr ? s_r[tid] : 0u;
     // window starts: frame t opens windows (r_{t-1} / W, r_t / W]  (W >= the longest frame)
     if (tid < nfr)
@@ -1665,6 +1674,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         s_ord[b + rank] = tid;
     }
     __syncthreads();
+    PB_LAP(3, tt);
 
     for (uint32_t w = 0; w < nwin; ++w)
     {
@@ -1728,10 +1738,12 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                     const int hi = last ? (int)(fend - 16u * mm) : 16;
                     if (lo > 0 || hi < 16)
                     {
-                        o0 &= pb_range_mask(lo, hi);
-                        o1 &= pb_range_mask(lo - 4, hi - 4);
-                        o2 &= pb_range_mask(lo - 8, hi - 8);
-                        o3 &= pb_range_mask(lo - 12, hi - 12);
+                        // keep bytes [lo, hi): two table rows instead of four clamped 64-bit shift pairs
+                        const pb_u32x4 ml = s_m16[lo], mh = s_m16[hi];
+                        o0 &= ml[0] & ~mh[0];
+                        o1 &= ml[1] & ~mh[1];
+                        o2 &= ml[2] & ~mh[2];
+                        o3 &= ml[3] & ~mh[3];
                     }
                     if (L4)
                         acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
@@ -1829,27 +1841,41 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             }
         }
         __syncthreads();
+        PB_LAP(2, tt);
 
         // ---------------- S: stage -> HBM, contiguous 16-B stores, then zero ----------------
         // the window's bytes [R0, R1) clipped to the workgroup's [lo, hi): whole chunks
         // [cf0, cf1); a chunk the window shares with a neighbouring window (same
         // workgroup) is byte-masked, stored by the lane that then zeroes it
+        // A chunk shared with the next window of this workgroup is not stored here: its value
+        // is carried into the next window's stage chunk 0 (the same 16 B of output) and stored
+        // whole with that window (masked byte stores by one lane per window edge made S ~25%
+        // of a workgroup's life).  Only workgroup edges (128-B aligned unless PBGPU_FST_DBG bit 6)
+        // and the launch's end keep masked stores.
         const uint32_t R0c = R0 > lo_rel ? R0 : lo_rel, R1c = R1 < hi_rel ? R1 : hi_rel;
         uint32_t cf0 = 0, cf1 = 0;
         uint8_t *const gout = K.out + wbase + sbase;
+        bool cout = false;
+        uint32_t chc = 0;
+        pb_u32x4 cv = pb_u32x4{0u, 0u, 0u, 0u};
         if (R0c < R1c)
         {
             const uint32_t lo_b = R0c - sbase, hi_b = R1c - sbase;
             const uint32_t cl = lo_b >> 4, ch = hi_b >> 4;
-            cf0 = (lo_b + 15u) >> 4;
+            const bool cin = w > 0 && R0c == R0 && (lo_b & 15u); // chunk cl holds the previous window's tail
+            cout = w + 1u < nwin && R1c == R1 && (hi_b & 15u);
+            chc = ch;
+            cf0 = cin ? cl : (lo_b + 15u) >> 4;
             cf1 = ch;
-            if ((lo_b & 15u) && tid == (cl & (PB_WG - 1u)))
+            if (cout && tid == (ch & (PB_WG - 1u)))
+                cv = stage[ch];
+            if ((lo_b & 15u) && !cin && tid == (cl & (PB_WG - 1u)))
             {
                 const pb_u32x4 v = stage[cl];
                 pb_store_chunk(gout + 16 * cl, v[0], v[1], v[2], v[3], (int)(16 * cl) - (int)lo_b,
                                (int)(hi_b - lo_b));
             }
-            if ((hi_b & 15u) && !((lo_b & 15u) && cl == ch) && tid == (ch & (PB_WG - 1u)))
+            if ((hi_b & 15u) && !cout && !((lo_b & 15u) && !cin && cl == ch) && tid == (ch & (PB_WG - 1u)))
             {
                 const pb_u32x4 v = stage[ch];
                 pb_store_chunk(gout + 16 * ch, v[0], v[1], v[2], v[3], (int)(16 * ch) - (int)lo_b,
@@ -1867,7 +1893,18 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             stage[c] = pb_u32x4{0u, 0u, 0u, 0u};
         }
         __syncthreads(); // the next window reuses the (zeroed) stage
+        if (cout && tid == (chc & (PB_WG - 1u)))
+        {
+            // ORed like every shared chunk, so it commutes with the next window's own ORs
+            uint32_t *const q = reinterpret_cast<uint32_t *>(stage);
+            atomicOr(q + 0, cv[0]);
+            atomicOr(q + 1, cv[1]);
+            atomicOr(q + 2, cv[2]);
+            atomicOr(q + 3, cv[3]);
+        }
+        PB_LAP(4, tt);
     }
+    PB_STAMP(6);
     if (K.fixed_len && blockIdx.x == 0 && tid == 0)
     {
         atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
