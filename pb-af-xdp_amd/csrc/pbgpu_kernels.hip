@@ -1496,7 +1496,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     const uint64_t fe = f0 + nown;
     // (PBGPU_FST_DBG bit 6, A/B only: the round-1 edges at the frame starts, lines split)
     const uint64_t emask = (K.fst_dbg & 64u) ? ~0ull : ~127ull;
-    const uint32_t nsc = SB >> 4; // stage chunks
 
     // ---------------- A: one lane per slot; the stage starts zero ----------------
     // Slot j holds frame f0 - PB_VST_GHOSTS + j: the possible ghosts, then the own
@@ -1523,8 +1522,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     for (uint32_t i = 0; i < (PB_STAGE_L48 + PB_WG - 1) / PB_WG; ++i)
         if (tid + i * PB_WG < PB_STAGE_L48)
             l48v[i] = K.lcg48[tid + i * PB_WG];
-    for (uint32_t c = tid; c < nsc; c += PB_WG)
-        stage[c] = pb_u32x4{0u, 0u, 0u, 0u};
     const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
     const int64_t fj = fb + (int64_t)tid;
     const bool valid = tid < CAP && fj >= 0 && (uint64_t)fj < fe;
@@ -1747,16 +1744,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                     }
                     if (L4)
                         acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
-                    if (hi < 16) // shared with the next frame
-                    {
-                        uint32_t *q = reinterpret_cast<uint32_t *>(pp);
-                        atomicOr(q + 0, o0);
-                        atomicOr(q + 1, o1);
-                        atomicOr(q + 2, o2);
-                        atomicOr(q + 3, o3);
-                    }
-                    else
-                        *pp = pb_u32x4{o0, o1, o2, o3};
+                    // whole chunk, zeros outside [lo, hi): the header bytes (this frame's or, past
+                    // the frame's end, the next frame's) are ORed in after the barrier below
+                    *pp = pb_u32x4{o0, o1, o2, o3};
                 };
                 edge(m, p);
                 for (uint32_t i = 2; i < cnt; ++i)
@@ -1801,6 +1791,21 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                     hv[K.csum_dw - PB_VST_HV0] |= K.csum_hi ? (c << 16) : c;
                 }
             }
+            // a frame without payload: its last chunk (header bytes, then the next frame's) gets
+            // its plain write here, as every payload-ending chunk does in the loop above
+            if (lg == 0u && fend == hend && (hend & 15u))
+                stage[cf + nch - 1u] = pb_u32x4{0u, 0u, 0u, 0u};
+        }
+        // every chunk of the window holding payload has had its one plain write; the headers
+        // are ORed into the chunks they share with payload or with the previous frame
+        __syncthreads();
+        for (uint32_t k = sb + grp0; k < (K.fst_dbg & 1u ? sb : se); k += NGW)
+        {
+            const uint32_t fr = s_ord[k];
+            const uint32_t r = s_r[fr] - sbase;
+            const uint32_t s0 = r & 15u, cf = r >> 4;
+            const uint32_t hend = s0 + hl;
+            const uint32_t *const hv = s_hv + fr * PB_VST_HVN;
             // header chunks 0 .. nhc-1: the image shifted to byte s0 (the image is zero past hl);
             // the first is shared with the previous frame unless s0 == 0, the last with the
             // payload (or the next frame) unless the header ends on the chunk edge
@@ -1886,22 +1891,13 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             cf1 = cf0;
         // (one chunk per step: four LDS reads in flight, then four stores, measured 1.7%
         // slower on configs[2])
-        for (uint32_t c = tid; c < nsc; c += PB_WG)
-        {
-            if (c >= cf0 && c < cf1)
-                pb_st16(gout + 16 * c, stage[c]);
-            stage[c] = pb_u32x4{0u, 0u, 0u, 0u};
-        }
-        __syncthreads(); // the next window reuses the (zeroed) stage
+        for (uint32_t c = cf0 + ((tid - cf0) & (PB_WG - 1u)); c < cf1; c += PB_WG)
+            pb_st16(gout + 16 * c, stage[c]);
+        __syncthreads(); // the next window reuses the stage
+        // the carried chunk is the next window's chunk 0: a header chunk there (ORed after that
+        // window's payload barrier), never a payload chunk, so this plain write is its first
         if (cout && tid == (chc & (PB_WG - 1u)))
-        {
-            // ORed like every shared chunk, so it commutes with the next window's own ORs
-            uint32_t *const q = reinterpret_cast<uint32_t *>(stage);
-            atomicOr(q + 0, cv[0]);
-            atomicOr(q + 1, cv[1]);
-            atomicOr(q + 2, cv[2]);
-            atomicOr(q + 3, cv[3]);
-        }
+            stage[0] = cv;
         PB_LAP(4, tt);
     }
     PB_STAMP(6);
