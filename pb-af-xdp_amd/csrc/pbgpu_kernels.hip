@@ -1658,7 +1658,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         const uint32_t w = my_r / W;
         const uint32_t b = s_win[w], e = s_win[w + 1];
         uint32_t rank = tid - b;
-        if (e - b <= 64)
+        if (e - b <= 64 && !(K.fst_dbg & 256u))
         {
             const uint32_t len = s_len[tid];
             rank = 0;
