@@ -1155,8 +1155,9 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     int rc = PBGPU_OK;
     if (!span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
         return rc;
-    const bool timing = K.stage_win && !K.fst_g && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
-    const uint64_t n_wg = K.stage_wgf ? (nf + K.stage_wgf - 1) / K.stage_wgf : 0;
+    const bool timing = (K.stage_win || K.fst_g) && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
+    const uint32_t wg_frames = K.fst_g ? K.fst_wgf : K.stage_wgf;
+    const uint64_t n_wg = wg_frames ? (nf + wg_frames - 1) / wg_frames : 0;
     if (timing)
     {
         if (ctx->dbg_cap < n_wg)

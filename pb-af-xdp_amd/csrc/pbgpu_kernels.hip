@@ -1265,6 +1265,10 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
     const uint32_t tid = threadIdx.x;
     const uint32_t flags = K.flags;
     const uint32_t flen = K.fixed_len, hl = K.hl;
+    unsigned long long tt = 0; // PB_TIMING builds: phase stamps (slot 1 A, 2 B, 4 S)
+    PB_STAMP(0);
+    if (PB_TIMING)
+        tt = __builtin_amdgcn_s_memtime();
     const uint64_t f0 = (uint64_t)blockIdx.x * WF;
     const uint64_t left = K.n_frames - f0;
     const uint32_t nfr = left < WF ? (uint32_t)left : WF;
@@ -1327,6 +1331,7 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
         }
     }
     __syncthreads();
+    PB_LAP(1, tt);
 
     const uint32_t nwin = (nfr + NGW - 1) / NGW;
     const uint32_t hw = hl >> 2; // header dwords written whole; hl % 4 == 2: one more half dword
@@ -1392,6 +1397,7 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
                 *reinterpret_cast<uint16_t *>(hp) = (uint16_t)v;
         }
         __syncthreads();
+        PB_LAP(2, tt);
 
         // ---------------- S: the window to HBM, contiguous 16-B stores ----------------
         // window bytes [0, R1); a last chunk that is not whole (the launch's last,
@@ -1427,7 +1433,9 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
             __syncthreads(); // the next window reuses the stage
         else
             sb = sb ? 0u : SB;
+        PB_LAP(4, tt);
     }
+    PB_STAMP(6);
     if (blockIdx.x == 0 && tid == 0)
     {
         atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
