@@ -1841,7 +1841,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                 for (int t = 0; t < 4; ++t)
                     h[t] = __builtin_amdgcn_alignbyte(wv[t + 1], wv[t], sh);
                 pb_u32x4 *p = stage + cf + lg;
-                if ((lg == 0 && s0) || (lg + 1u == nhc && (hend & 15u)))
+                // (the workgroup's first frame has no predecessor built here: its chunk 0 is
+                // written plain, zeros before the frame, bytes another workgroup stores)
+                if ((lg == 0 && s0 && fr > 0u) || (lg + 1u == nhc && (hend & 15u)))
                 {
                     uint32_t *q = reinterpret_cast<uint32_t *>(p);
                     atomicOr(q + 0, h[0]);

@@ -49,6 +49,17 @@ SHAPES = [
     ("vstage_no32", {"PBGPU_FST_DBG": "32"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
+    # the other correct-output switches: workgroup edges at frame starts (lines split between
+    # workgroups, masked stores at every edge), natural window order, the 3-pass offsets scan
+    ("vstage_split_edges", {"PBGPU_FST_DBG": "64"},
+     ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
+      "pb_xpage_kernel", "pb_gpf_kernel")),
+    ("vstage_no_order", {"PBGPU_FST_DBG": "256"},
+     ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
+      "pb_xpage_kernel", "pb_gpf_kernel")),
+    ("vstage_3pass_kb8", {"PBGPU_VST_SCAN": "3pass", "PBGPU_STAGE_KB": "8"},
+     ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
+      "pb_xpage_kernel", "pb_gpf_kernel")),
 ]
 
 # pb_fstage_kernel shapes (fixed lengths > 128 B, multiple of 4, random payload)
