@@ -1806,10 +1806,17 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         }
         // every chunk of the window holding payload has had its one plain write; the headers
         // are ORed into the chunks they share with payload or with the previous frame
+        // One lane per (frame, header chunk), frames in window order, mh = the most header
+        // chunks a frame can touch: ~F * mh lanes carry the pass (configs[2]: ~108 of 256), so
+        // the other waves skip it instead of running it with one live lane in two or three
         __syncthreads();
-        for (uint32_t k = sb + grp0; k < (K.fst_dbg & 1u ? sb : se); k += NGW)
+        const uint32_t mh = (hl + 30u) >> 4;
+        const uint32_t nhl = (K.fst_dbg & 1u) ? 0u : (se - sb) * mh;
+        for (uint32_t i = tid; i < nhl; i += PB_WG)
         {
-            const uint32_t fr = s_ord[k];
+            const uint32_t ti = mh == 4u ? (i >> 2) : i / mh;
+            const uint32_t lg = i - ti * mh;
+            const uint32_t fr = sb + ti;
             const uint32_t r = s_r[fr] - sbase;
             const uint32_t s0 = r & 15u, cf = r >> 4;
             const uint32_t hend = s0 + hl;
