@@ -1731,7 +1731,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             {
                 // edge chunks (the lane's first may be chunk ma, lane 0's last the frame's last)
                 // are masked in the first and last passes only; the passes between are plain
-                uint32_t m = mlast - (cnt - 1u) * g;
+                uint32_t m = mlast - __umul24(cnt - 1u, g);
                 const uint2 Mm = s_l48[m];
                 uint32_t x = __umul24(s_z[fr], Mm.x) + Mm.y;
                 pb_u32x4 *p = stage + cf + m;
@@ -1776,7 +1776,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                     edge(m, p);
                 }
             }
-            uint32_t *const hv = s_hv + fr * PB_VST_HVN;
+            uint32_t *const hv = s_hv + __umul24(fr, PB_VST_HVN);
             if (L4)
             {
                 if (G == 8)
@@ -1811,16 +1811,17 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         // the other waves skip it instead of running it with one live lane in two or three
         __syncthreads();
         const uint32_t mh = (hl + 30u) >> 4;
+        const uint32_t mhinv = (65536u + mh - 1u) / mh;
         const uint32_t nhl = (K.fst_dbg & 1u) ? 0u : (se - sb) * mh;
         for (uint32_t i = tid; i < nhl; i += PB_WG)
         {
-            const uint32_t ti = mh == 4u ? (i >> 2) : i / mh;
-            const uint32_t lg = i - ti * mh;
+            const uint32_t ti = __umul24(i, mhinv) >> 16; // i / mh (exact for i < 2^12, mh <= 8)
+            const uint32_t lg = i - __umul24(ti, mh);
             const uint32_t fr = sb + ti;
             const uint32_t r = s_r[fr] - sbase;
             const uint32_t s0 = r & 15u, cf = r >> 4;
             const uint32_t hend = s0 + hl;
-            const uint32_t *const hv = s_hv + fr * PB_VST_HVN;
+            const uint32_t *const hv = s_hv + __umul24(fr, PB_VST_HVN);
             // header chunks 0 .. nhc-1: the image shifted to byte s0 (the image is zero past hl);
             // the first is shared with the previous frame unless s0 == 0, the last with the
             // payload (or the next frame) unless the header ends on the chunk edge
