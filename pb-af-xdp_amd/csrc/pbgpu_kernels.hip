@@ -1692,6 +1692,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         // window's longest frames (s_ord is longest first) take 32 / 16 lanes: y frames of
         // 32, then x of 16, then 8 each, groups aligned to their size
         uint32_t g = G, grp0 = tid / G, lg = tid % G;
+        bool any32 = false; // (workgroup-uniform) a 32-lane group exists in this window
         // the layout's counts assume 256 lanes: 32 y + 16 x == 256 for 9-16 frames, 32 F <= 256 for F <= 8
         static_assert(PB_WG == 256, "pb_vstage_kernel's 32/16/8-lane window layout is for 256-thread workgroups");
         if (G == 8 && !(K.fst_dbg & 16u))
@@ -1705,6 +1706,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             }
             else if (F <= 32u)
                 x = 32u - F;
+            any32 = y > 0u;
             if (tid < 32u * y)
                 g = 32, grp0 = tid >> 5, lg = tid & 31u;
             else if (tid < 32u * y + 16u * x)
@@ -1784,8 +1786,12 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                     // sums over 8, 16 and 32 lanes; each lane keeps its own group's
                     const uint32_t a8 = pb_group_sum<8>(acc);
                     const uint32_t a16 = a8 + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a8, 0x128, 0xF, 0xF, false);
-                    const uint32_t a32 = a16 + __shfl_xor(a16, 16, 64);
-                    acc = g == 8 ? a8 : (g == 16 ? a16 : a32);
+                    acc = g == 8 ? a8 : a16;
+                    if (any32) // the cross-row step (an LDS permute) only for windows that use it
+                    {
+                        const uint32_t a32 = a16 + __shfl_xor(a16, 16, 64);
+                        acc = g == 32 ? a32 : acc;
+                    }
                 }
                 else
                     acc = pb_group_sum<G>(acc);
