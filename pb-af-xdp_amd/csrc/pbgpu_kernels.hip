@@ -1447,17 +1447,19 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
 //
 // Packed variable-length frames (configs[2]) and fixed lengths that are not a
 // multiple of 4: pb_stage_kernel's windows (frames starting in bytes
-// [w W, (w + 1) W) of the workgroup's output), with the per-frame work cut:
-//  * the stage is zero before a window is built (S zeroes what it streamed), so
-//    a chunk two frames share (a frame's last chunk = the next frame's first) is
-//    assembled with LDS ORs of each frame's own bytes, in any order; every other
-//    chunk belongs to one frame and is a plain 16-B write;
-//  * the group writes its frame's header itself once its checksum is known (the
-//    header image shifted to the frame's byte offset, ORed into the chunks it
-//    shares with the payload / the previous frame): no header pass and no
-//    barrier between payload and headers;
-//  * the first payload chunk's header bytes and the last chunk's bytes past the
-//    frame are masked in the payload loop, so phase A has no serial byte loops.
+// [w W, (w + 1) W) of the workgroup's output), with the per-frame work cut
+// (DESIGN.md 5.4a):
+//  * phase A: one lane per slot (up to 4 earlier "ghost" frames, then the own
+//    frames), lengths from the seeds, starts from a workgroup scan on top of one
+//    offset; per frame only header dwords 4-12 in LDS, the rest from the template;
+//  * payload pass: g lanes per frame (8/16/32 by window), every chunk holding payload
+//    written once and plain (zeros outside the frame), edge chunks masked from a
+//    table; the L4 sum reduced over the group and written into the frame's record;
+//  * barrier, then a header pass with one lane per (frame, header chunk), ORing the
+//    header into the chunks it shares with payload or with the previous frame;
+//  * S: the window's chunks to HBM; the chunk shared with the next window is carried
+//    into that window's stage chunk 0 instead of being stored twice, byte-masked;
+//    the stage is never cleared.
 // Lane lg of a group takes chunks nch-1-lg, nch-1-lg-G, ... as in pb_fstage_kernel.
 template <int G, bool L4>
 __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
