@@ -59,6 +59,7 @@ struct pb_pl
     uint32_t blob_off; // static bytes at blob + blob_off (16-B zero pad around)
     uint32_t slen;     // static length
     uint32_t ssum;     // static bytes' little-endian 16-bit word sum (unfolded)
+    uint32_t lit_stop; // literal rule, several payloads: min { j > i : setup data_len[j] <= j } (<= 64)
 };
 
 struct pb_kargs

@@ -634,8 +634,14 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             bytes.assign(len, 0);
             if (R.payload_rule == PB_PAYLOAD_LITERAL)
             {
+                // the shadowed index runs while j < data_len[j], which may pass the payload's
+                // own length: those draws still advance the seed, their bytes are not sent
                 for (uint32_t j = 0; j < PB_MAX_PAYLOADS && j < dl_setup[j]; ++j)
-                    bytes[j] = (uint8_t)host_rand_r(&sseed);
+                {
+                    const uint8_t v = (uint8_t)host_rand_r(&sseed);
+                    if (j < len)
+                        bytes[j] = v;
+                }
             }
             else
             {
@@ -681,8 +687,18 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         P.blob_off = 16 + 64;
         pls.push_back(P);
     }
-    if ((flags & PBK_LITERAL) && pls.size() > 1 && n_random > 0)
-        return PBGPU_ENOTSUP; // history-dependent quirk (B8): oracle only
+    // literal rule with several payloads (quirk B8, sequence.c:349 / 552): a random payload's
+    // loop `for (u16 i = 0; i < data_len[i]; i++)` reads the other payloads' data_len[]
+    // entries, so it draws until the first j with data_len[j] <= j.  Entries j > i hold
+    // their setup values (declared rule, as the oracle); their part of the stop index is
+    // fixed per payload here, the part of j <= i is found per iteration in pb_payload.
+    for (size_t i = 0; i < pls.size(); ++i)
+    {
+        uint32_t j = (uint32_t)i + 1;
+        while (j < PB_MAX_PAYLOADS && j < dl_setup[j])
+            ++j;
+        pls[i].lit_stop = j;
+    }
     if ((flags & PBK_LITERAL) || max_random <= 64)
         flags |= PBK_SUM_IN_A;
 

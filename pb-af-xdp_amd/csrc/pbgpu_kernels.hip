@@ -76,6 +76,31 @@ __device__ __forceinline__ pb_frame_pl pb_payload(const pb_kargs &K, uint32_t s,
 {
     if (K.pl_cnt == 1)
         return pb_payload_of(K.pl0, s, K.flags);
+    if (K.flags & PBK_LITERAL)
+    {
+        // literal rule, several payloads (sequence.c:545-556, quirk B8): payload p draws
+        // rand_r while j < data_len[j], i.e. up to the first j with data_len[j] <= j:
+        // j < p this iteration's lengths (first such j kept in `m`), j == p its own
+        // draw, j > p the setup values (lit_stop, from pbgpu_load_sequence).  Only
+        // random payloads draw; the bytes past the payload's length are not sent.
+        uint32_t cur = s, m = 0xFFFFu;
+        for (uint32_t p = 0;; ++p)
+        {
+            const pb_pl &Q = K.pls[p];
+            const uint32_t len = Q.random ? Q.min_len + pb_mod(pb_rand_r(cur), Q.len) : Q.slen;
+            const uint32_t nv = min(min(m, Q.lit_stop), len <= p ? p : 0xFFFFu);
+            if (p == i)
+            {
+                pb_frame_pl r = pb_payload_of(Q, cur, 0u);
+                r.nvalid = Q.random ? min(nv, len) : Q.slen;
+                return r;
+            }
+            if (Q.random)
+                cur = pb_jump(K, cur, nv);
+            if (m == 0xFFFFu && len <= p)
+                m = p;
+        }
+    }
     // earlier random payloads advance the seed by one rand_r per byte
     uint32_t cur = s;
     for (uint32_t p = 0; p < i; ++p)

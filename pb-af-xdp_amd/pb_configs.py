@@ -149,6 +149,14 @@ def _edge_cases():
                      {"isstatic": 1, "length": {"min": 5, "max": 40}}, {"exact": "hello, world", "isstring": 1}]
     e["udp_multi_payload"] = c
 
+    # several short payloads: under the literal rule each random one draws until the first
+    # j with data_len[j] <= j (quirk B8), which these lengths make land anywhere in 0..6
+    c = c2_udp_64()
+    c["payloads"] = [{"length": {"min": 0, "max": 3}}, {"exact": "ab cd"}, {"length": {"min": 1, "max": 6}},
+                     {"isstatic": 1, "length": {"min": 2, "max": 4}}, {"length": {"min": 0, "max": 40}},
+                     {"length": {"min": 5, "max": 5}}]
+    e["udp_multi_short"] = c
+
     c = c2_udp_64()
     c["payloads"] = [{"length": {"min": 2000, "max": 16000}}]
     e["udp_jumbo_var"] = c
@@ -175,6 +183,8 @@ RULE_CASES = [
     ("c3_udp_var", 1, 0),
     ("udp_rnd_ttl_id_tos", 0, 1),  # single-fold IPv4 checksum
     ("c4_tcp_syn", 1, 1),
+    ("udp_multi_payload", 1, 0),   # literal rule, several payloads (B8)
+    ("udp_multi_short", 1, 0),
 ]
 
 

@@ -148,7 +148,8 @@ def build(cfg, seq_idx, first_iter, n_iter, seed_base, literal=False, single_fol
             if literal:
                 while j < len(dl) and j < dl[j]:
                     r, ss = rand_r(ss)
-                    buf[j] = r & 0xFF
+                    if j < n:
+                        buf[j] = r & 0xFF
                     j += 1
             else:
                 for j in range(n):
@@ -194,7 +195,8 @@ def build(cfg, seq_idx, first_iter, n_iter, seed_base, literal=False, single_fol
                     j = 0
                     while j < len(dl) and j < dl[j]:
                         r, s = rand_r(s)
-                        buf[j] = r & 0xFF
+                        if j < n:
+                            buf[j] = r & 0xFF
                         j += 1
                 else:
                     for j in range(n):

@@ -233,9 +233,6 @@ def test_error_behaviour(ctx):
     with pytest.raises(pbgpu.PbError) as e:
         ctx.load_sequence(1, Sequence.from_config(nodst), 1)
     assert e.value.code == -22
-    with pytest.raises(pbgpu.PbError) as e:
-        ctx.load_sequence(1, Sequence.from_config(pc.get("udp_multi_payload")), 1, payload_rule=1)
-    assert e.value.code == -95
 
 
 def test_fill_probe_runs(ctx):
