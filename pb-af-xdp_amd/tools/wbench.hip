@@ -266,6 +266,31 @@ __global__ __launch_bounds__(256) void fill_stride(uint8_t *dst, uint32_t ppw, u
     }
 }
 
+// Half-chip ownership probe: does the 4 KiB XCD-residue effect come from one
+// memory unit per XCD, or from the half of the chip (IOD) an XCD sits on?
+// Workgroup b (XCD x = b % 8, the k = b / 8-th of that XCD) writes one block of
+// `bpp` consecutive 4 KiB pages; the blocks alternate between two page-residue
+// halves ({0..3}, {4..7} for bpp = 4), and XCD x writes only half grp(x):
+//   group 0: grp = x / 4   group 1: grp = x % 2   group 2: grp = (x / 2) % 2
+// the XCD's rank j in its half picks the block: block = (k * 4 + j) * 2 + grp.
+template <int WG>
+__global__ __launch_bounds__(WG) void fill_half(uint8_t *dst, uint32_t bpp, uint32_t group)
+{
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint32_t x = b & 7u, k = b >> 3;
+    uint32_t grp, j;
+    if (group == 0)
+        grp = x >> 2, j = x & 3u;
+    else if (group == 1)
+        grp = x & 1u, j = x >> 1;
+    else
+        grp = (x >> 1) & 1u, j = (x & 1u) | ((x >> 2) << 1);
+    const uint64_t blk = ((uint64_t)k * 4 + j) * 2 + grp;
+    const uint64_t base = blk * bpp * 4096ull;
+    for (uint32_t q = t; q < bpp * 256u; q += WG)
+        st16<false>(dst + base + 16ull * q, u32x4{b, q, 2u, 3u});
+}
+
 // Kernel timing: best of 3 trials, each the mean of `reps` back-to-back launches
 // after one untimed launch.
 template <typename F>
@@ -523,6 +548,31 @@ int main(int argc, char **argv)
                 snprintf(nm, sizeof nm, "stride pages=%u stride=%u", ppw, S);
                 rep(nm, (uint64_t)grid * 4096 * ppw,
                     timeit([&] { hipLaunchKernelGGL(fill_stride, dim3(grid), dim3(256), 0, 0, buf, ppw, S); }, 20));
+            }
+    }
+    if (want(argc, argv, "half"))
+    {
+        // one XCD-owned page per workgroup (the reference shape), then 8 / 16 KiB blocks by half
+        {
+            const uint32_t grid = (uint32_t)(g_bytes / 4096 / 8 * 8);
+            rep("half baseline xcd page wg=256", (uint64_t)grid * 4096,
+                timeit([&] { hipLaunchKernelGGL(fill_stride, dim3(grid), dim3(256), 0, 0, buf, 1u, 8u); }, 20));
+        }
+        for (uint32_t bpp : {2u, 4u})
+            for (uint32_t group : {0u, 1u, 2u})
+            {
+                const uint32_t grid = (uint32_t)(g_bytes / (4096ull * bpp) / 8 * 8);
+                char nm[96];
+                snprintf(nm, sizeof nm, "half bpp=%u group=%u wg=256", bpp, group);
+                rep(nm, (uint64_t)grid * 4096 * bpp,
+                    timeit([&] { hipLaunchKernelGGL(fill_half<256>, dim3(grid), dim3(256), 0, 0, buf, bpp, group); }, 20));
+                snprintf(nm, sizeof nm, "half bpp=%u group=%u wg=%u", bpp, group, 256 * bpp);
+                if (bpp == 2)
+                    rep(nm, (uint64_t)grid * 4096 * bpp,
+                        timeit([&] { hipLaunchKernelGGL(fill_half<512>, dim3(grid), dim3(512), 0, 0, buf, bpp, group); }, 20));
+                else
+                    rep(nm, (uint64_t)grid * 4096 * bpp,
+                        timeit([&] { hipLaunchKernelGGL(fill_half<1024>, dim3(grid), dim3(1024), 0, 0, buf, bpp, group); }, 20));
             }
     }
     if (want(argc, argv, "memset"))
