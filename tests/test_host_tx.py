@@ -27,9 +27,13 @@ STUB = os.path.join(BUILD, "libpbhost_stub.so")
 @pytest.fixture(scope="module")
 def libs():
     os.makedirs(BUILD, exist_ok=True)
-    subprocess.run(["gcc", "-O2", "-Wall", "-shared", "-fPIC", "-pthread", "-o", STUB,
+    # built under a per-process name and renamed into place, so parallel test workers
+    # (pytest -n) never load a half-written library
+    tmp = f"{STUB}.{os.getpid()}"
+    subprocess.run(["gcc", "-O2", "-Wall", "-shared", "-fPIC", "-pthread", "-o", tmp,
                     os.path.join(ROOT, "tests", "host_stub.c"), "-L" + LIBDIR, "-lpbhost",
                     "-Wl,-rpath," + LIBDIR], check=True)
+    os.replace(tmp, STUB)
     host = C.CDLL(os.path.join(LIBDIR, "libpbhost.so"))
     stub = C.CDLL(STUB)
     host.seq_send.argtypes = [C.c_char_p, SequenceT, C.c_uint16, OurCmd]
@@ -328,8 +332,16 @@ def test_non_blocking_sequences_run_concurrently(libs):
     host.seq_send(b"lo", a.c, 3, _cmd(host, gpu_batch=1000))
     t_first = time.perf_counter() - t0
     host.seq_send(b"lo", b.c, 3, _cmd(host, gpu_batch=1000))
-    host.pb_shutdown_stats(None)
     p0, p1 = C.c_uint64(), C.c_uint64()
+    # the paced sequence is still running: wait (bounded) for its first frames, so a
+    # loaded machine cannot stop it before its thread has sent anything
+    t1 = time.perf_counter() + 10.0
+    while time.perf_counter() < t1:
+        host.pb_sequence_totals(0, C.byref(p0), None)
+        if p0.value:
+            break
+        time.sleep(0.005)
+    host.pb_shutdown_stats(None)
     host.pb_sequence_totals(0, C.byref(p0), None)
     host.pb_sequence_totals(1, C.byref(p1), None)
     assert t_first < 0.5
