@@ -59,7 +59,6 @@ struct pb_pl
     uint32_t blob_off; // static bytes at blob + blob_off (16-B zero pad around)
     uint32_t slen;     // static length
     uint32_t ssum;     // static bytes' little-endian 16-bit word sum (unfolded)
-    uint32_t lit_stop; // literal rule, several payloads: min { j > i : setup data_len[j] <= j } (<= 64)
 };
 
 struct pb_kargs
@@ -136,6 +135,10 @@ struct pb_kargs
     const uint32_t *vblk_sum;
     const unsigned long long *vblk_l2;
     uint64_t *offsets_w;
+    // (appended last: the fields above keep their kernel-argument offsets)
+    // literal rule, several payloads: lit_stop[i] = min { j > i : setup data_len[j] <= j } (<= 64)
+    const uint32_t *lit_stop;
+    uint32_t small_wgt;     // pb_small_kernel's threads (= frames) per workgroup: 256 (0), 128 or 64
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

@@ -96,6 +96,7 @@ struct seq_slot
     uint32_t min_flen = 0, max_flen = 0;
     uint2 *d_ranges = nullptr;
     pb_pl *d_pls = nullptr;
+    uint32_t *d_lit_stop = nullptr;
     uint8_t *d_blob = nullptr;
 };
 
@@ -333,6 +334,8 @@ void slot_free(seq_slot &s)
         (void)hipFree(s.d_ranges);
     if (s.d_pls)
         (void)hipFree(s.d_pls);
+    if (s.d_lit_stop)
+        (void)hipFree(s.d_lit_stop);
     if (s.d_blob)
         (void)hipFree(s.d_blob);
     s = seq_slot();
@@ -692,12 +695,13 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     // entries, so it draws until the first j with data_len[j] <= j.  Entries j > i hold
     // their setup values (declared rule, as the oracle); their part of the stop index is
     // fixed per payload here, the part of j <= i is found per iteration in pb_payload.
+    std::vector<uint32_t> lit_stop(pls.size());
     for (size_t i = 0; i < pls.size(); ++i)
     {
         uint32_t j = (uint32_t)i + 1;
         while (j < PB_MAX_PAYLOADS && j < dl_setup[j])
             ++j;
-        pls[i].lit_stop = j;
+        lit_stop[i] = j;
     }
     if ((flags & PBK_LITERAL) || max_random <= 64)
         flags |= PBK_SUM_IN_A;
@@ -728,6 +732,14 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     if (fixed && pls.size() == 1 && minf <= 128)
     {
         K.small_ndw = minf <= 64 ? 16 : 32;
+        {
+            // the linear small kernel's frames per workgroup: 64 for even lengths (their 64-frame
+            // regions end on 128-B lines), measured 2.5% faster than 256 on the 98-B ICMP frame
+            // (0.649 vs 0.666 ms per 2^25 frames; 128: 0.666; profiles/r02/ab/small_wgt_icmp98.txt);
+            // odd lengths keep 256 (line-aligned regions).  PBGPU_SMALL_WGT = 64 / 128 / 256 overrides
+            const int w = env_int("PBGPU_SMALL_WGT", minf % 2 == 0 ? 64 : 256);
+            K.small_wgt = (w == 64 || w == 128) ? (uint32_t)w : 0u;
+        }
         const bool xp_force = env_is("PBGPU_XP_FORCE", "1"); // experiments: pb_xpage_kernel for any length % 4 == 0
         if (4096 % minf == 0 && !xp_force) // pages of whole frames: pb_xsmall_kernel
         {
@@ -951,11 +963,14 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         return rc;
     if ((rc = upload(&S.d_pls, pls.data(), pls.size())) != PBGPU_OK)
         return rc;
+    if ((rc = upload(&S.d_lit_stop, lit_stop.data(), lit_stop.size())) != PBGPU_OK)
+        return rc;
     blob.insert(blob.end(), 64, 0);
     if ((rc = upload(&S.d_blob, blob.data(), blob.size())) != PBGPU_OK)
         return rc;
     K.ranges = S.d_ranges;
     K.pls = S.d_pls;
+    K.lit_stop = S.d_lit_stop;
     K.blob = S.d_blob;
     K.jump = ctx->d_jump;
     K.lcg48 = ctx->d_lcg48;
@@ -1630,11 +1645,12 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
+    else if (K.xs_np && !env_is("PBGPU_KERNEL", "linear"))
+        snprintf(buf, n, "%s<%u, %u, %s>", K.xp ? "pb_xpage_kernel" : "pb_xsmall_kernel", K.small_ndw, K.proto,
+                 K.pl0.random ? "true" : "false");
     else
-        snprintf(buf, n, "%s<%u, %u, %s>",
-                 K.xs_np && !env_is("PBGPU_KERNEL", "linear") ? (K.xp ? "pb_xpage_kernel" : "pb_xsmall_kernel")
-                                                               : "pb_small_kernel",
-                 K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
+        snprintf(buf, n, "pb_small_kernel<%u, %u, %s, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
+                 K.small_wgt ? K.small_wgt : (uint32_t)PB_WG);
     return PBGPU_OK;
 }
 

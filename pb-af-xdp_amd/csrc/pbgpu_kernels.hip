@@ -72,23 +72,24 @@ __device__ __forceinline__ pb_frame_pl pb_payload_of(const pb_pl &P, uint32_t cu
 // record is read in place (kernel argument or device table): a local copy chosen
 // from either became a stack object, 16 B of scratch stores per lane per
 // workgroup (~4% of the staged kernels' HBM writes, PMC WRITE_SIZE).
+template <bool LIT = true> // false: kernels that never run the literal rule (no dead loop in them)
 __device__ __forceinline__ pb_frame_pl pb_payload(const pb_kargs &K, uint32_t s, uint32_t i)
 {
     if (K.pl_cnt == 1)
         return pb_payload_of(K.pl0, s, K.flags);
-    if (K.flags & PBK_LITERAL)
+    if (LIT && (K.flags & PBK_LITERAL))
     {
         // literal rule, several payloads (sequence.c:545-556, quirk B8): payload p draws
         // rand_r while j < data_len[j], i.e. up to the first j with data_len[j] <= j:
         // j < p this iteration's lengths (first such j kept in `m`), j == p its own
-        // draw, j > p the setup values (lit_stop, from pbgpu_load_sequence).  Only
+        // draw, j > p the setup values (K.lit_stop, from pbgpu_load_sequence).  Only
         // random payloads draw; the bytes past the payload's length are not sent.
         uint32_t cur = s, m = 0xFFFFu;
         for (uint32_t p = 0;; ++p)
         {
             const pb_pl &Q = K.pls[p];
             const uint32_t len = Q.random ? Q.min_len + pb_mod(pb_rand_r(cur), Q.len) : Q.slen;
-            const uint32_t nv = min(min(m, Q.lit_stop), len <= p ? p : 0xFFFFu);
+            const uint32_t nv = min(min(m, K.lit_stop[p]), len <= p ? p : 0xFFFFu);
             if (p == i)
             {
                 pb_frame_pl r = pb_payload_of(Q, cur, 0u);
@@ -129,13 +130,14 @@ __device__ __forceinline__ void pb_frame_index(const pb_kargs &K, uint64_t f, ui
     }
 }
 
+template <bool LIT = true>
 __device__ __forceinline__ uint32_t pb_frame_len(const pb_kargs &K, uint64_t f)
 {
     uint64_t k;
     uint32_t i;
     pb_frame_index(K, f, k, i);
     const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
-    return K.hl + pb_payload(K, s, i).plen;
+    return K.hl + pb_payload<LIT>(K, s, i).plen;
 }
 
 // keep bytes [lo, hi) of dword t (byte positions 4t .. 4t+3)
@@ -453,17 +455,17 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
     }
 }
 
-// Linear form: workgroup b builds frames [256 b, 256 b + 256) and writes their
-// contiguous byte range.  Used when the output is not 4 KiB aligned (and under
+// Linear form: workgroup b builds frames [WGT b, WGT b + WGT) and writes their
+// contiguous byte range (WGT = 256, or 128 / 64: smaller regions per workgroup).  Used when the output is not 4 KiB aligned (and under
 // PBGPU_KERNEL=linear for comparison).
-template <int NDW, int PROTO, bool RANDOM>
-__global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
+template <int NDW, int PROTO, bool RANDOM, int WGT>
+__global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_tile[PB_WG * NDW + 8];
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[WGT * NDW + 8];
     const uint32_t tid = threadIdx.x;
-    const uint64_t f0 = (uint64_t)blockIdx.x * PB_WG;
+    const uint64_t f0 = (uint64_t)blockIdx.x * WGT;
     const uint64_t left = K.n_frames - f0;
-    const uint32_t nfr = left < PB_WG ? (uint32_t)left : PB_WG;
+    const uint32_t nfr = left < WGT ? (uint32_t)left : WGT;
     const uint32_t flen = K.fixed_len;
 
     if (tid < nfr)
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(PB_WG) void pb_small_kernel(pb_kargs K)
     const uint32_t nchunks = (tile_bytes + 15) >> 4;
     uint8_t *const out = K.out + f0 * flen;
     const bool swz = (flen & 7u) == 0;
-    for (uint32_t c = tid; c < nchunks; c += PB_WG)
+    for (uint32_t c = tid; c < nchunks; c += WGT)
     {
         pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[swz ? pb_swz(c) : c];
         if (16 * c + 16 > tile_bytes) // last chunk of the stream: zero the tail
@@ -1328,7 +1330,7 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
         pb_frame_index(K, f, k, pi);
         const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
         const uint32_t r0 = pb_rand_r(s);
-        const pb_frame_pl P = pb_payload(K, s, pi);
+        const pb_frame_pl P = pb_payload<false>(K, s, pi);
         uint32_t d[16];
         const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
         pb_u32x4 *row = reinterpret_cast<pb_u32x4 *>(s_img + tid * 16);
@@ -1569,7 +1571,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         pb_frame_index(K, (uint64_t)fj, k, pi);
         const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
         const uint32_t r0 = pb_rand_r(s);
-        const pb_frame_pl P = pb_payload(K, s, pi);
+        const pb_frame_pl P = pb_payload<false>(K, s, pi);
         const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
         flen = K.fixed_len ? K.fixed_len : hl + P.plen;
         st0 = P.st0;
@@ -2145,14 +2147,32 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
         if (K->xs_grid)
             hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
         else
-            hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true>), dim3(grid), dim3(PB_WG), K->lds_pad, st, *K);
+        {
+            const uint32_t wgt = K->small_wgt ? K->small_wgt : PB_WG;
+            const uint32_t g = (uint32_t)((K->n_frames + wgt - 1) / wgt);
+            if (wgt == 64)
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, 64>), dim3(g), dim3(64), K->lds_pad, st, *K);
+            else if (wgt == 128)
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, 128>), dim3(g), dim3(128), K->lds_pad, st, *K);
+            else
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, PB_WG>), dim3(g), dim3(PB_WG), K->lds_pad, st, *K);
+        }
     }
     else
     {
         if (K->xs_grid)
             hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
         else
-            hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false>), dim3(grid), dim3(PB_WG), K->lds_pad, st, *K);
+        {
+            const uint32_t wgt = K->small_wgt ? K->small_wgt : PB_WG;
+            const uint32_t g = (uint32_t)((K->n_frames + wgt - 1) / wgt);
+            if (wgt == 64)
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, 64>), dim3(g), dim3(64), K->lds_pad, st, *K);
+            else if (wgt == 128)
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, 128>), dim3(g), dim3(128), K->lds_pad, st, *K);
+            else
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, PB_WG>), dim3(g), dim3(PB_WG), K->lds_pad, st, *K);
+        }
     }
 }
 
@@ -2311,7 +2331,7 @@ __global__ __launch_bounds__(256) void pb_len_wgsum(pb_kargs K, uint32_t wgf, ui
         const uint64_t fz = fa + wgf < K.n_frames ? fa + wgf : K.n_frames;
 #pragma unroll 4
         for (uint64_t f = fa; f < fz; ++f)
-            sum += pb_frame_len(K, f);
+            sum += pb_frame_len<false>(K, f);
         bsum[b] = sum;
     }
     unsigned long long v = sum;

@@ -147,7 +147,8 @@ XS_LENS = [42, 43, 44, 48, 52, 56, 60, 64, 72, 96, 98, 100, 106, 108, 116, 120, 
 XS_COUNTS = [1, 5, 200, 2048, 2049, 2 * 2048 * 5 + 77]
 
 
-@pytest.mark.parametrize("force_xpage", [False, True, 512], ids=["default", "xpage_forced", "xpage_forced_512"])
+@pytest.mark.parametrize("force_xpage", [False, True, 512, "lin64", "lin128"],
+                         ids=["default", "xpage_forced", "xpage_forced_512", "linear_wg64", "linear_wg128"])
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
 @pytest.mark.parametrize("flen", XS_LENS)
 def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
@@ -155,6 +156,11 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
         monkeypatch.setenv("PBGPU_XP_FORCE", "1")
     if force_xpage == 512:
         monkeypatch.setenv("PBGPU_XP_WGT", "512")
+    lin = force_xpage in ("lin64", "lin128")
+    if lin:  # the linear small kernel at 64 / 128 frames per workgroup, for every length
+        monkeypatch.delenv("PBGPU_XP_FORCE", raising=False)
+        monkeypatch.setenv("PBGPU_KERNEL", "linear")
+        monkeypatch.setenv("PBGPU_SMALL_WGT", force_xpage[3:])
     hl = 54 if proto == "tcp" else 42
     if flen < hl or (proto == "icmp" and flen == hl):
         pytest.skip("shorter than the headers / empty static payload")
@@ -167,7 +173,9 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
         n = max(1, n * 64 // flen)  # page counts as named above at every length
         kern = _check(ctx, cfg, 1000003 + n, n)
         xp_default = flen <= 64 and 512 // ((4096 + flen - 1) // flen + 1) >= 6
-        if flen % 4 == 0 and (force_xpage or (4096 % flen and xp_default)):
+        if lin:
+            want = "pb_small_kernel<"
+        elif flen % 4 == 0 and (force_xpage or (4096 % flen and xp_default)):
             want = "pb_xpage_kernel"
         else:
             want = "pb_xsmall_kernel" if 4096 % flen == 0 else "pb_small_kernel<"
