@@ -291,6 +291,44 @@ __global__ __launch_bounds__(WG) void fill_half(uint8_t *dst, uint32_t bpp, uint
         st16<false>(dst + base + 16ull * q, u32x4{b, q, 2u, 3u});
 }
 
+// Persistent grid-stride windows: `grid` workgroups (about one resident set)
+// loop over windows g = b, b + grid, ... of wb bytes each (the byte offset of
+// window g is g * wb, so wb need not be a multiple of 128: windows then split
+// lines between workgroups), staged in LDS with a barrier per window as the
+// staged kernels do.  At any moment the resident workgroups write neighbouring
+// windows: the concurrent write footprint is ~grid * wb, against grid * (a
+// workgroup's whole region) for contiguous per-workgroup regions.
+__global__ __launch_bounds__(256) void fill_gwin(uint8_t *dst, uint32_t wb, uint64_t nwin)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    for (uint64_t g = b; g < nwin; g += gridDim.x)
+    {
+        const uint64_t w0 = g * wb;
+        const uint32_t c0 = (uint32_t)(w0 & 15u);          // window start inside its first chunk
+        const uint32_t nc = (c0 + wb + 15u) >> 4;
+        for (uint32_t q = t; q < nc; q += 256)
+            reinterpret_cast<u32x4 *>(lds)[q] = u32x4{(uint32_t)g, q, 2u, 3u};
+        __syncthreads();
+        uint8_t *const base = dst + (w0 & ~15ull);
+        for (uint32_t q = t; q < nc; q += 256)
+        {
+            const u32x4 v = reinterpret_cast<const u32x4 *>(lds)[q];
+            if ((q == 0 && c0) || (q == nc - 1 && ((c0 + wb) & 15u)))
+            {
+                // edge chunk shared with the neighbouring window: its own dwords only
+                const int lo = q == 0 ? (int)c0 : 0, hi = q == nc - 1 && ((c0 + wb) & 15u) ? (int)((c0 + wb) & 15u) : 16;
+                uint32_t *w = reinterpret_cast<uint32_t *>(base + 16ull * q);
+                for (int i = lo / 4; i < hi / 4; ++i)
+                    w[i] = v[i];
+            }
+            else
+                st16<false>(base + 16ull * q, v);
+        }
+        __syncthreads();
+    }
+}
+
 // Kernel timing: best of 3 trials, each the mean of `reps` back-to-back launches
 // after one untimed launch.
 template <typename F>
@@ -573,6 +611,24 @@ int main(int argc, char **argv)
                 else
                     rep(nm, (uint64_t)grid * 4096 * bpp,
                         timeit([&] { hipLaunchKernelGGL(fill_half<1024>, dim3(grid), dim3(1024), 0, 0, buf, bpp, group); }, 20));
+            }
+    }
+    if (want(argc, argv, "gwin"))
+    {
+        // staged windows, persistent grid-stride vs contiguous per-workgroup regions
+        // (fill_win mode 0 at 4 windows per workgroup); 1500-B-frame windows: 16 frames
+        // (24,000 B, edges split lines) and 32 frames (48,000 B, line-aligned)
+        for (uint32_t wb : {24576u, 24000u, 48000u, 16384u, 8192u})
+            for (uint32_t wpc : {5u, 4u, 3u})
+            {
+                const uint32_t lds = 163840u / wpc - 512u < 65536u ? 163840u / wpc - 512u : 65536u;
+                if (lds < wb + 16)
+                    continue;
+                const uint64_t nwin = (g_bytes - 65536) / wb;
+                const uint32_t grid = 256u * wpc;
+                char nm[96];
+                snprintf(nm, sizeof nm, "gwin wb=%u grid=%u (%u per CU)", wb, grid, wpc);
+                rep(nm, nwin * wb, timeit([&] { hipLaunchKernelGGL(fill_gwin, dim3(grid), dim3(256), lds, 0, buf, wb, nwin); }, 20));
             }
     }
     if (want(argc, argv, "memset"))
