@@ -45,7 +45,7 @@ extern "C" {
 #define PBGPU_EINVAL (-22)    /* bad config (e.g. min > max, no dst_ip) */
 #define PBGPU_ENOSPC (-28)    /* frames buffer too small */
 #define PBGPU_ENODEV (-19)    /* no such GPU */
-#define PBGPU_ENOTSUP (-95)   /* valid config this build does not run on the GPU */
+#define PBGPU_ENOTSUP (-95)   /* reserved: a valid config this build would not run on the GPU (none since round 2) */
 
 typedef struct pbgpu_ctx pbgpu_ctx;
 
