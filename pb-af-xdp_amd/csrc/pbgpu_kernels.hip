@@ -85,22 +85,21 @@ __device__ __forceinline__ pb_frame_pl pb_payload(const pb_kargs &K, uint32_t s,
         // draw, j > p the setup values (K.lit_stop, from pbgpu_load_sequence).  Only
         // random payloads draw; the bytes past the payload's length are not sent.
         uint32_t cur = s, m = 0xFFFFu;
-        for (uint32_t p = 0;; ++p)
+        for (uint32_t p = 0; p < i; ++p)
         {
             const pb_pl &Q = K.pls[p];
             const uint32_t len = Q.random ? Q.min_len + pb_mod(pb_rand_r(cur), Q.len) : Q.slen;
             const uint32_t nv = min(min(m, K.lit_stop[p]), len <= p ? p : 0xFFFFu);
-            if (p == i)
-            {
-                pb_frame_pl r = pb_payload_of(Q, cur, 0u);
-                r.nvalid = Q.random ? min(nv, len) : Q.slen;
-                return r;
-            }
             if (Q.random)
                 cur = pb_jump(K, cur, nv);
             if (m == 0xFFFFu && len <= p)
                 m = p;
         }
+        const pb_pl &Q = K.pls[i];
+        pb_frame_pl r = pb_payload_of(Q, cur, 0u);
+        if (Q.random)
+            r.nvalid = min(min(min(m, K.lit_stop[i]), r.plen <= i ? i : 0xFFFFu), r.plen);
+        return r;
     }
     // earlier random payloads advance the seed by one rand_r per byte
     uint32_t cur = s;
