@@ -92,6 +92,24 @@ def test_json_config_sequences_equal_oracle(tmp_path):
     assert read_pcap(pcap) == want
 
 
+def test_json_config_literal_multi_payload_equals_oracle(tmp_path):
+    """--literal with a sequence of six short payloads (static, exact and random):
+    under the literal rule each random payload draws until the first j with
+    data_len[j] <= j (quirk B8, sequence.c:545-556); the capture equals the oracle's
+    frames under the same rule, six frames per iteration."""
+    c = dict(pc.get("udp_multi_short"))
+    c.update({"maxpckts": 6 * 700, "delay": 0, "block": 1})
+    path = tmp_path / "lit.json"
+    path.write_text(json.dumps({"interface": "pbnodev0", "sequences": [c]}))
+    pcap = tmp_path / "lit.pcap"
+    r = subprocess.run([BIN, "-c", str(path), "--gpubatch", "256", "--seed", "31", "--literal", "--pcap", str(pcap)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    want = ob.frames(Sequence.from_config(c), 0, 0, 700, 31, payload_rule=1)
+    assert len(want) == 6 * 700
+    assert read_pcap(pcap) == want
+
+
 def test_cli_two_threads_send_distinct_iterations(tmp_path):
     """--threads 2 on one GPU (sequence.c:741: one TX thread per queue, here two
     pbgpu contexts on one GPU): the max_pckts quota is split exactly and every
