@@ -302,7 +302,7 @@ static void *gpu_worker(void *p)
     while (batch > 1 && batch * fpi * max_flen > PB_BATCH_BYTES_MAX)
         batch >>= 1;
     /* launch-level pacing: one launch covers at most ~1/10 s of the configured rate
-     * (pps, bps and pps are global over the sequence's threads; delay is per thread
+     * (pps and bps are global over the sequence's threads; delay is per thread
      * and per packet, sequence.c:655-659) */
     if (seq->pps > 0)
     {
