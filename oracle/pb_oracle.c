@@ -793,3 +793,86 @@ int pbo_build_mt(const pb_sequence_t *seq, const uint8_t *smac, const uint8_t *d
     free(st);
     return rc;
 }
+
+/* ---------------- checker: every frame's checksums (test infrastructure) ----------------
+ * RFC 1071 verification of packed frames (Ethernet + IPv4 without options + UDP / TCP /
+ * ICMP), independent of how they were built: the IPv4 header words and the L4 segment
+ * words (plus the pseudo header for UDP / TCP, sequence.c:585-602) each fold to 0xFFFF,
+ * and tot_len equals the frame length - 14.  Used by the full-size GPU tests, whose
+ * frames are too many to compare one by one with the oracle. */
+static uint32_t sum16_be(const uint8_t *p, uint32_t len)
+{
+    uint32_t s = 0;
+    uint32_t i = 0;
+    for (; i + 1 < len; i += 2)
+        s += (uint32_t)p[i] << 8 | p[i + 1];
+    if (i < len)
+        s += (uint32_t)p[i] << 8;
+    return s;
+}
+
+static uint32_t fold16(uint64_t s)
+{
+    while (s >> 16)
+        s = (s & 0xFFFF) + (s >> 16);
+    return (uint32_t)s;
+}
+
+static int verify_one(const uint8_t *f, uint32_t len)
+{
+    if (len < 34)
+        return 1;
+    if (fold16(sum16_be(f + 14, 20)) != 0xFFFF)
+        return 1;
+    if (((uint32_t)f[16] << 8 | f[17]) != len - 14)
+        return 1;
+    const uint8_t proto = f[23];
+    uint64_t s = sum16_be(f + 34, len - 34);
+    if (proto == 6 || proto == 17)
+        s += sum16_be(f + 26, 8) + proto + (len - 34);
+    return fold16(s) != 0xFFFF;
+}
+
+typedef struct verify_job
+{
+    const uint8_t *data;
+    const uint64_t *off;
+    uint32_t flen;
+    uint64_t a, b, bad;
+} verify_job_t;
+
+static void *verify_worker(void *arg)
+{
+    verify_job_t *j = (verify_job_t *)arg;
+    for (uint64_t i = j->a; i < j->b; i++)
+    {
+        const uint64_t s = j->off ? j->off[i] - j->off[0] : i * (uint64_t)j->flen;
+        const uint32_t len = j->off ? (uint32_t)(j->off[i + 1] - j->off[i]) : j->flen;
+        j->bad += (uint64_t)verify_one(j->data + s, len);
+    }
+    return NULL;
+}
+
+uint64_t pbo_verify_frames(const uint8_t *data, const uint64_t *offsets, uint32_t fixed_len, uint64_t n,
+                           int nthreads)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    verify_job_t jobs[256];
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; t++)
+    {
+        jobs[t] = (verify_job_t){data, offsets, fixed_len, n * (uint64_t)t / (uint64_t)nthreads,
+                                 n * (uint64_t)(t + 1) / (uint64_t)nthreads, 0};
+        pthread_create(&th[t], NULL, verify_worker, &jobs[t]);
+    }
+    uint64_t bad = 0;
+    for (int t = 0; t < nthreads; t++)
+    {
+        pthread_join(th[t], NULL);
+        bad += jobs[t].bad;
+    }
+    return bad;
+}

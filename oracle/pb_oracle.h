@@ -67,6 +67,12 @@ int pbo_build_mt(const pb_sequence_t *seq, const uint8_t *smac, const uint8_t *d
 uint16_t pbo_iph_csum(const uint8_t *iph20, int single_fold);
 uint16_t pbo_l4_csum(const uint8_t *l4, uint32_t len, uint32_t saddr_be, uint32_t daddr_be, uint8_t proto);
 
+/* Checker: the number of frames whose IPv4 checksum, tot_len or L4 checksum does not
+ * verify.  Frame i is data[offsets[i] - offsets[0], offsets[i + 1] - offsets[0]), or
+ * fixed_len bytes at i * fixed_len when offsets is NULL. */
+uint64_t pbo_verify_frames(const uint8_t *data, const uint64_t *offsets, uint32_t fixed_len, uint64_t n,
+                           int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,8 @@ def lib():
         L.pbo_iph_csum.argtypes = [C.c_char_p, C.c_int]
         L.pbo_l4_csum.restype = C.c_uint16
         L.pbo_l4_csum.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint8]
+        L.pbo_verify_frames.restype = C.c_uint64
+        L.pbo_verify_frames.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int]
         _lib = L
     return _lib
 
@@ -105,3 +107,10 @@ def build_slots_mt(seq, seq_idx, first_iter, n_iter, seed_base, nthreads, slot=4
     if rc != 0:
         raise RuntimeError(f"pbo_build_mt -> {rc}")
     return out, int(tot.value)
+
+
+def verify_frames(data: np.ndarray, offsets, fixed_len: int, n: int, nthreads: int = 16) -> int:
+    """Frames among n whose IPv4 checksum, tot_len or L4 checksum fails (C checker)."""
+    off = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    return int(lib().pbo_verify_frames(data.ctypes.data, None if off is None else off.ctypes.data, fixed_len, n,
+                                       nthreads))

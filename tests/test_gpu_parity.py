@@ -127,6 +127,38 @@ def test_full_size_properties(ctx, name, n_iter):
         assert frames[int(k)].tobytes() == want
 
 
+@pytest.mark.parametrize("name", ["c2_udp_1500", "c3_udp_var", "c5_icmp_echo"])
+def test_full_size_every_checksum(ctx, name):
+    """SURVEY.md §8d sizes (2^25 iterations, 50 GB of 1500-B frames, 27.6 GB of packed
+    configs[2] frames): every frame's IPv4 checksum, tot_len and L4 checksum verify,
+    checked in host chunks by the C checker (pbo_verify_frames, RFC 1071 over the frame
+    bytes); configs[2]'s offsets are a prefix sum of lengths in [106, 1542]."""
+    seq = Sequence.from_config(pc.get(name))
+    n = 1 << 25
+    ctx.load_sequence(0, seq, pc.SEED_BASE)
+    mf, mb = ctx.build_size(0, n)
+    fb = ctx.alloc_frames(mf, mb)
+    try:
+        ctx.build(0, 0, n, fb)
+        ctx.sync()
+        flen = int(fb.f.fixed_len)
+        off = None if flen else fb.offsets()
+        if off is not None:
+            lens = np.diff(off.astype(np.int64))
+            assert off[0] == 0 and lens.min() >= 106 and lens.max() <= 1542
+        ch = 1 << 21
+        buf = np.empty(ch * (flen or 1542), dtype=np.uint8)
+        bad = 0
+        for lo in range(0, n, ch):
+            hi = min(n, lo + ch)
+            b0, b1 = (lo * flen, hi * flen) if flen else (int(off[lo]), int(off[hi]))
+            assert ctx.lib.pbgpu_copy_packed(ctx.h, fb.ptr, buf.ctypes.data, b0, b1 - b0) == 0
+            bad += ob.verify_frames(buf, None if flen else off[lo:hi + 1], flen, hi - lo, 16)
+        assert bad == 0
+    finally:
+        fb.free()
+
+
 def test_variable_full_size_offsets(ctx):
     """configs[2] at 2^22 frames: offsets are a prefix sum of lengths in
     [106, 1542], every sampled frame equals the oracle's, every checksum verifies."""

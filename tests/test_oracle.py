@@ -114,3 +114,26 @@ def test_single_fold_differs_only_on_carry():
     a = ob.lib().pbo_iph_csum(h, 0)
     b = ob.lib().pbo_iph_csum(h, 1)
     assert a != b and a == struct.unpack("<H", struct.pack("!H", pv.inet_csum(h)))[0]
+
+
+def test_frame_checker_on_reference_kats_and_oracle_frames():
+    """pbo_verify_frames (the full-size GPU tests' checker) accepts the reference's captured
+    frames and every BASELINE / edge config's oracle frames that carry both checksums, and
+    rejects a frame with one flipped bit in the IPv4 header, the L4 header or the payload."""
+    import pb_configs as pc
+
+    for _, want in kat_cases():
+        a = np.frombuffer(want, dtype=np.uint8).copy()
+        assert ob.verify_frames(a, None, len(want), 1, 1) == 0
+    for name in pc.ALL:
+        cfg = pc.get(name)
+        if cfg.get("l4csum", 1) == 0 or cfg["ip"].get("csum", 1) == 0 or "jumbo" in name:
+            continue
+        seq = Sequence.from_config(cfg)
+        data, off = ob.build(seq, 0, 0, 300, pc.SEED_BASE)
+        n = len(off) - 1
+        assert ob.verify_frames(data, off, 0, n, 4) == 0, name
+        for pos in (16, 24, 36, int(off[1]) - 1):  # tot_len, IPv4 csum, L4 header, last byte of frame 0
+            bad = data.copy()
+            bad[pos] ^= 0x10
+            assert ob.verify_frames(bad, off, 0, n, 4) == 1, (name, pos)
