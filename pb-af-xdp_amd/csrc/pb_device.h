@@ -149,6 +149,19 @@ struct pb_kargs
 #define PB_VST_PRO 576 // pb_vstage_kernel prologue records: 16 jump entries, 12 starts / S0 parts, 4 wave sums, template, 17 chunk masks (16-B multiple)
 #define PB_VST_HV0 4u  // per-frame header dwords kept in LDS: [4, 13) = IPv4 from tot_len to the L4 checksum
 #define PB_VST_HVN 9u  // (UDP csum dword 10, TCP 12, ICMP 9); dwords 0-3 and 13-15 are the template's
+// each XCD builds one contiguous eighth of a launch's workgroup regions (pb_xcd_region)
+#ifndef PB_FST_XREMAP
+#define PB_FST_XREMAP 1
+#endif
+#ifndef PB_VST_XREMAP
+#define PB_VST_XREMAP 1
+#endif
+#ifndef PB_SMALL_XREMAP
+#define PB_SMALL_XREMAP 0 // measured: no change for 98-B / 106-B frames
+#endif
+#ifndef PB_XS_XREMAP
+#define PB_XS_XREMAP 0
+#endif
 #define PB_VST_CAP(wgf) (((size_t)(wgf) + PB_VST_GHOSTS + 1) & ~(size_t)1)
 #define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + PB_VST_PRO + PB_VST_CAP(wgf) * (PB_VST_HVN + 5) * 4 + (PB_VST_CAP(wgf) + 2) * 4)
 
