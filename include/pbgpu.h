@@ -149,12 +149,13 @@ int pbgpu_set_timing(pbgpu_ctx *ctx, int mode);
 int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches);
 /* Write-only roofline probe: `reps` launches (best of two trials) of each of
  * PBGPU_FILL_SHAPES fill shapes over `bytes` — 16-B stores per lane at 16 / 4 /
- * 8 KiB per workgroup, plain and non-temporal, workgroups per CU capped by LDS,
+ * 8 KiB per workgroup, plain and non-temporal, workgroups per CU capped by LDS, linear or
+ * XCD-contiguous workgroup regions,
  * and the runtime's hipMemsetD32Async (tools/wbench.hip found the fastest plain
  * fills).  pbgpu_fill_probe returns the fastest shape's mean
  * device time per launch; _ex returns every shape's and the fastest's index,
  * pbgpu_fill_shape_name names a shape. */
-#define PBGPU_FILL_SHAPES 9
+#define PBGPU_FILL_SHAPES 12
 int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_launch);
 int pbgpu_fill_probe_ex(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_shape, int *best_shape);
 const char *pbgpu_fill_shape_name(int shape);

@@ -21,7 +21,7 @@
 #define PB_LCG48_N 4200                    // lcg48[m] = L^(48 m), m < 4200 (> 16-B chunks of a 64 KiB frame)
 #define PB_XPG 4096                        // XCD-owned page bytes (pb_xsmall_kernel, pb_xpage_kernel)
 #define PB_XREG (PB_XPG + 256)             // LDS bytes per page region (128 B slack either side)
-#define PBK_FILL_SHAPES 9                  // write-roofline probe shapes (pbk_launch_fill)
+#define PBK_FILL_SHAPES 12                 // write-roofline probe shapes (pbk_launch_fill)
 #define PB_XNP_MAX 8                       // pb_xsmall_kernel: pages per workgroup, 4 (64-B frames) or 8 (128-B)
 
 // glibc LCG

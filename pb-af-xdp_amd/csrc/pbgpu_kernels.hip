@@ -2121,10 +2121,10 @@ __global__ __launch_bounds__(256) void pb_scatter_fixed(const uint8_t *src, uint
 // write-only roofline probe: each workgroup streams PER contiguous 4-KiB sweeps
 // of 16-B stores (PER = 4: the linear build kernels' shape; PER = 1: 4 KiB per
 // workgroup, the fastest plain fill measured, tools/wbench.hip)
-template <bool NT, int PER>
+template <bool NT, int PER, bool XR = false> // XR: XCD-contiguous regions (pb_xcd_region)
 __global__ __launch_bounds__(256) void pb_fill_kernel(pb_u32x4 *dst, uint64_t n16, uint32_t v)
 {
-    const uint64_t b = (uint64_t)blockIdx.x * (256 * PER);
+    const uint64_t b = (uint64_t)(XR ? pb_xcd_region(blockIdx.x, gridDim.x) : blockIdx.x) * (256 * PER);
 #pragma unroll
     for (int i = 0; i < PER; ++i)
     {
@@ -2412,12 +2412,15 @@ __global__ __launch_bounds__(512) void pb_fill512_kernel(pb_u32x4 *dst, uint64_t
 //  2  4 KiB per workgroup, one plain store per lane (8 / CU)  6  4 KiB, 3 workgroups / CU
 //  3  4 KiB, LDS-capped at 6 workgroups / CU                 7  8 KiB per 512-thread workgroup, 1 store / lane
 //  8  hipMemsetD32Async (the runtime's fill)
+//  9-11  shapes 0, 2 and 5 with XCD-contiguous regions (each XCD fills its own eighth, as the
+//        staged build kernels write since pb_xcd_region)
 extern "C" const char *pbk_fill_shape_name(int mode)
 {
     static const char *names[PBK_FILL_SHAPES] = {
         "16KiB/wg 4 st/lane", "16KiB/wg 4 st/lane nt", "4KiB/wg 1 st/lane (8 wg/CU)", "4KiB/wg 1 st/lane, 6 wg/CU",
         "4KiB/wg 1 st/lane, 5 wg/CU", "4KiB/wg 1 st/lane, 4 wg/CU", "4KiB/wg 1 st/lane, 3 wg/CU",
-        "8KiB/512-thread wg 1 st/lane", "hipMemsetD32Async"};
+        "8KiB/512-thread wg 1 st/lane", "hipMemsetD32Async", "16KiB/wg 4 st/lane, XCD-contiguous",
+        "4KiB/wg 1 st/lane (8 wg/CU), XCD-contiguous", "4KiB/wg 1 st/lane, 4 wg/CU, XCD-contiguous"};
     return mode >= 0 && mode < PBK_FILL_SHAPES ? names[mode] : "?";
 }
 
@@ -2445,6 +2448,15 @@ extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipSt
     case 7:
         hipLaunchKernelGGL(pb_fill512_kernel, dim3((uint32_t)((n16 + 511) / 512)), dim3(512), 0, st, (pb_u32x4 *)dst,
                            n16, 0x5A5A5A5Au);
+        break;
+    case 9:
+        hipLaunchKernelGGL((pb_fill_kernel<false, 4, true>), dim3(g4), dim3(256), 0, st, (pb_u32x4 *)dst, n16,
+                           0x5A5A5A5Au);
+        break;
+    case 10:
+    case 11:
+        hipLaunchKernelGGL((pb_fill_kernel<false, 1, true>), dim3(g1), dim3(256), mode == 10 ? 0u : cap_lds[2], st,
+                           (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
         break;
     default:
         return hipMemsetD32Async((hipDeviceptr_t)dst, 0x5A5A5A5Au, bytes / 4, st);
