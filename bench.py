@@ -94,7 +94,7 @@ def barrier(dist, local):
         torch.cuda.synchronize(local)
 
 
-def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ramp_s=0.0):
+def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ramp_s=0.0, launch_reps=0):
     """Warm up, then time exactly `steps` steps; a step builds `n_pkts` iterations
     of every sequence in `names` (one launch each).  Returns per-rank timings and
     the all-reduced counters of the timed steps.
@@ -137,14 +137,39 @@ def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ram
     p1, b1 = ctx.counters(nseq)
     dp = [int(x) for x in (p1 - p0)]
     db = [int(x) for x in (b1 - b0)]
+    # the kernels count the frames they built and the bytes they stored, workgroup by
+    # workgroup: a short or skipped build fails here instead of inflating the rate
+    for i in range(nseq):
+        flen = int(bufs[i].f.fixed_len)
+        if dp[i] != steps * n_pkts or (flen and db[i] != steps * n_pkts * flen):
+            raise SystemExit(f"counter mismatch on {names[i]}: {dp[i]} frames / {db[i]} bytes for "
+                             f"{steps} x {n_pkts} iterations")
     counters = None
     if dist is not None:
         # RCCL over xGMI: the global sent-packet / byte counters of the timed steps
         gp, gb = pb_dist.allreduce_counters(dp, db, device=f"cuda:{local}")
         counters = {"packets": gp, "bytes": gb}
+        if gp != [steps * n_pkts * world] * nseq:
+            raise SystemExit(f"global counter mismatch: {gp} frames for {world} x {steps} x {n_pkts} per sequence")
     barrier(dist, local)
     wall = time.perf_counter() - t0
     k_ms, k_n = ctx.kernel_time()
+    # a separate pass with an event pair around every launch: each launch's own device
+    # time (median / min / max; the pairs add ~10 us between launches, so `value` and
+    # the roofline come from the span above, not from this pass)
+    per_launch = None
+    if launch_reps:
+        ctx.set_timing(ctx.TIMING_LAUNCH)
+        for s in range(launch_reps):
+            step(warmup + steps + s)
+        ctx.sync()
+        t = ctx.kernel_times()
+        ctx.set_timing(ctx.TIMING_SPAN)
+        if len(t):
+            per_step = t.reshape(-1, nseq).sum(axis=1) if len(t) % nseq == 0 else t
+            per_launch = {"median": round(float(np.median(per_step)), 5), "min": round(float(per_step.min()), 5),
+                          "max": round(float(per_step.max()), 5), "n": int(len(per_step)),
+                          "mode": "HIP event pair around every launch, separate pass after the timed span"}
     flens = [int(fb.f.fixed_len) for fb in bufs]
     kernels = [ctx.kernel_name(i) for i in range(nseq)]
     for fb in bufs:
@@ -156,6 +181,7 @@ def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ram
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
     return {"wall_s": wall, "span_ms_per_step": k_ms / max(steps, 1), "kernel_launches": k_n, "flens": flens,
+            "per_launch_ms": per_launch,
             "counters": counters, "packets_per_step": sum(dp) // steps, "bytes_per_step": sum(db) // steps,
             "per_seq_bytes_per_step": [x // steps for x in db], "kernels": kernels}
 
@@ -206,15 +232,26 @@ def host_cpu():
             "cgroup_cpu_quota": quota}
 
 
+def usable_cpus():
+    """The CPUs this process can actually use: its affinity mask, capped by the
+    cgroup CPU quota (the GPU box gives a 16-CPU quota on a 256-CPU host, so 256
+    threads would only time-slice 16 CPUs' worth)."""
+    n = len(os.sched_getaffinity(0))
+    q = host_cpu()["cgroup_cpu_quota"]
+    if q:
+        n = min(n, int(-(-q // 1)))
+    return max(1, n)
+
+
 def cpu_baseline(name, budget_s, threads=None, faithful=True):
     """The CPU oracle on the host cores, frames copied into 4 KiB UMEM slots.
     faithful: a clock read and the rand_ip dotted-string round trip per
     iteration, as sequence.c:434-497 does; lean: integer only.
-    Default threads: every CPU this process may run on (sched_getaffinity)."""
+    Default threads: the usable CPUs (affinity mask capped by the cgroup quota)."""
     import oracle_binding as ob
 
     if threads is None:
-        threads = max(1, len(os.sched_getaffinity(0)))
+        threads = usable_cpus()
     seq = Sequence.from_config(pc.get(name))
     n = 20000 * threads
     ring = 4096  # NUM_FRAMES slots per socket, af_xdp.h:23
@@ -251,7 +288,8 @@ def main():
     dist, world, rank, local = init_dist(a.gpus)
     ctx = GpuContext(local)
     names = list(MIX) if a.config == "c5_mix" else [a.config]
-    res = run_configs(ctx, names, a.packets, a.steps, a.warmup, rank, world, dist, local, a.ramp_seconds)
+    res = run_configs(ctx, names, a.packets, a.steps, a.warmup, rank, world, dist, local, a.ramp_seconds,
+                      launch_reps=20)
     bps = res["bytes_per_step"]  # frame bytes one step builds on one GPU
     pkts_total = res["packets_per_step"] * a.steps * world
     wall = res["wall_s"]
@@ -267,14 +305,17 @@ def main():
         extra["write_peak_probe_shape"] = best
         extra["write_peak_probe_shapes_gbps"] = {k: round(bps / (v * 1e-3) / 1e9, 1) for k, v in shapes.items()}
     if not a.no_variants and a.config == "c2_udp_64":
-        steps15 = max(3, a.steps // 4)
-        v = run_configs(ctx, ["c2_udp_1500"], a.packets, steps15, 1, rank, world, dist, local, a.ramp_seconds / 2)
+        # >= 20 timed steps (~0.15 s of 50-GB launches) after a full clock ramp
+        steps15 = max(20, a.steps // 4)
+        v = run_configs(ctx, ["c2_udp_1500"], a.packets, steps15, 2, rank, world, dist, local, a.ramp_seconds,
+                        launch_reps=20)
         n1500 = v["packets_per_step"] * steps15 * world
         ach15 = v["bytes_per_step"] / (v["span_ms_per_step"] * 1e-3) / 1e9
         extra["udp_1500"] = {
             "mpps": round(n1500 / v["wall_s"] / 1e6, 3),
             "gbps": round(v["bytes_per_step"] * steps15 * world / v["wall_s"] / 1e9, 2),
-            "kernel": v["kernels"][0], "kernel_ms_avg": round(v["span_ms_per_step"], 4),
+            "steps": steps15, "kernel": v["kernels"][0], "kernel_ms_avg": round(v["span_ms_per_step"], 4),
+            "per_launch_ms": v["per_launch_ms"],
             "roofline_achieved_gbps": round(ach15, 1), "roofline_frac": round(ach15 / HBM_PEAK_GBPS, 4),
             "frac_of_guide_achievable": round(ach15 / HBM_ACHIEVABLE_GBPS, 4),
             "frac_of_measured_write_peak": round(ach15 / peak_probe, 4) if peak_probe else None,
@@ -320,6 +361,7 @@ def main():
                      "traffic": pmc_traffic(a.pmc, names, a.packets), "traffic_source": os.path.relpath(a.pmc, ROOT),
                      "kernel": res["kernels"][0] if len(names) == 1 else res["kernels"],
                      "kernel_ms_avg": round(res["span_ms_per_step"], 5),
+                     "per_launch_ms": res["per_launch_ms"],
                      "algorithmic_bytes_per_launch": bps},
     }
     if res["counters"] is not None:
@@ -334,7 +376,8 @@ def main():
         short = max(1.0, a.cpu_seconds / 4)
         line["cpu_baseline_variants"] = {
             "faithful_1_thread": cpu_baseline(names[0], short, threads=1),
-            "lean_all_threads": cpu_baseline(names[0], short, faithful=False),
+            "faithful_16_threads": cpu_baseline(names[0], short, threads=16),
+            "lean_usable_threads": cpu_baseline(names[0], short, faithful=False),
             "configs0_c1_udp_static_64_1_thread": dict(
                 cpu_baseline("c1_udp_static_64", short, threads=1),
                 af_xdp_send="not measured: no AF_XDP socket / CAP_NET_RAW on the GPU host (BASELINE.md §3)")}

@@ -122,15 +122,21 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *frames, void *umem, u
 /* The same, asynchronous: returns once the landing is queued (registered UMEM;
  * unregistered memory lands synchronously).  lens_out must stay valid until
  * pbgpu_land_wait() returns for it: that call waits until at most `keep`
- * landings are still queued, oldest first, and fills their lens_out. */
+ * landings are still queued, oldest first, and fills their lens_out.
+ * A later pbgpu_build() into the same frames buffer is ordered after the
+ * landings queued from it (the build stream waits on the last one), so a
+ * caller may rebuild a buffer without waiting; builds into other buffers
+ * overlap the landing. */
 int pbgpu_copy_to_umem_async(pbgpu_ctx *ctx, const pbgpu_frames *frames, void *umem, uint32_t slot_stride,
                              uint32_t first_slot, uint64_t first_frame, uint32_t n, uint16_t *lens_out);
 int pbgpu_land_wait(pbgpu_ctx *ctx, uint32_t keep);
 int pbgpu_host_register(pbgpu_ctx *ctx, void *ptr, size_t bytes);
 int pbgpu_host_unregister(pbgpu_ctx *ctx, void *ptr);
 
-/* ---- counters (sequence.c:12-14, 633-642): frames / bytes built per
- * sequence since open; multi-GPU callers all-reduce these over RCCL. ---- */
+/* ---- counters (sequence.c:12-14, 633-642): frames built / bytes stored per
+ * sequence since open, added by the build kernels' workgroups as they finish
+ * their share (a skipped or short build shows here); multi-GPU callers
+ * all-reduce these over RCCL. ---- */
 int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq);
 
 /* ---- measurement ---- */
@@ -147,6 +153,9 @@ int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq);
 #define PBGPU_TIMING_SPAN 1
 int pbgpu_set_timing(pbgpu_ctx *ctx, int mode);
 int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches);
+/* PBGPU_TIMING_LAUNCH only: each launch's own device time since the last call
+ * (the first `cap` of them into ms_each, oldest first) and the launch count. */
+int pbgpu_kernel_times(pbgpu_ctx *ctx, double *ms_each, uint32_t cap, uint32_t *n_launches);
 /* Write-only roofline probe: `reps` launches (best of two trials) of each of
  * PBGPU_FILL_SHAPES fill shapes over `bytes` — 16-B stores per lane at 16 / 4 /
  * 8 KiB per workgroup, plain and non-temporal, workgroups per CU capped by LDS, linear or

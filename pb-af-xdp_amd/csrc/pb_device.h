@@ -23,6 +23,8 @@
 #define PB_XREG (PB_XPG + 256)             // LDS bytes per page region (128 B slack either side)
 #define PBK_FILL_SHAPES 12                 // write-roofline probe shapes (pbk_launch_fill)
 #define PB_XNP_MAX 8                       // pb_xsmall_kernel: pages per workgroup, 4 (64-B frames) or 8 (128-B)
+#define PB_CTR_SHARDS 64                   // per-sequence counter shards (workgroup b adds to shard b % 64)
+#define PB_CTR_STRIDE 16                   // u64 words per shard: one 128-B line each ({frames, bytes} + pad)
 
 // glibc LCG
 #define PB_LCG_A 1103515245u

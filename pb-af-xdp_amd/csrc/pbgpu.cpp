@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <new>
 #include <deque>
 #include <vector>
 
@@ -37,6 +38,8 @@ extern "C" hipError_t pbk_launch_scatter_fixed(const uint8_t *src, uint32_t flen
 #define PB_JUMP_N (65536 + 256) // entries j = -PB_JNEG .. 65536 + 175
 #define PB_SCAN_FRAMES_PER_BLOCK (256 * 8)
 #define PB_VST_SCAN_MIN_WGF 32 // smallest pb_vstage_kernel workgroup the scratch is sized for
+#define PB_CTR_WORDS ((size_t)PB_CTR_SHARDS * PB_CTR_STRIDE) // u64 counter words per sequence
+#define PB_CTR_BYTES (sizeof(unsigned long long) * PB_CTR_WORDS * PB_MAX_SEQUENCES)
 
 // device scratch of a frames buffer: the 3-pass length scan's block sums, or pb_vstage_kernel's
 // per-workgroup length sums (u32) + their per-256 group sums (u64)
@@ -105,6 +108,23 @@ struct timing_pair
     hipEvent_t a, b;
 };
 
+// What pbgpu_frames.reserved points to: the buffer's build-completion event (the landing
+// stream waits on it) and the completion event of the last landing queued from it (the
+// next build into the buffer waits on that, so a landing never reads frames being rebuilt)
+struct frames_events
+{
+    hipEvent_t built = nullptr;
+    hipEvent_t landed = nullptr;
+    bool land_pending = false;
+};
+
+frames_events *frames_ev(pbgpu_frames *f)
+{
+    if (f->reserved == NULL)
+        f->reserved = new (std::nothrow) frames_events();
+    return (frames_events *)f->reserved;
+}
+
 } // namespace
 
 struct pbgpu_ctx
@@ -117,7 +137,7 @@ struct pbgpu_ctx
     uint2 *d_lcg48 = nullptr;
     unsigned long long *d_dbg = nullptr; // PBGPU_TIMING: per-workgroup phase stamps
     uint64_t dbg_cap = 0;
-    unsigned long long *d_counters = nullptr; // [PB_MAX_SEQUENCES][4]
+    unsigned long long *d_counters = nullptr; // [PB_MAX_SEQUENCES][PB_CTR_SHARDS][PB_CTR_STRIDE]
     seq_slot seqs[PB_MAX_SEQUENCES];
     std::vector<timing_pair> pending;
     std::vector<timing_pair> pool;
@@ -405,8 +425,8 @@ int pbgpu_open(int device, pbgpu_ctx **out)
         }
     }
     if (upload(&ctx->d_jump, jt.data(), jt.size()) != PBGPU_OK || upload(&ctx->d_lcg48, l48.data(), l48.size()) != PBGPU_OK ||
-        hipMalloc((void **)&ctx->d_counters, sizeof(unsigned long long) * 4 * PB_MAX_SEQUENCES) != hipSuccess ||
-        hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * 4 * PB_MAX_SEQUENCES) != hipSuccess)
+        hipMalloc((void **)&ctx->d_counters, PB_CTR_BYTES) != hipSuccess ||
+        hipMemset(ctx->d_counters, 0, PB_CTR_BYTES) != hipSuccess)
     {
         pbgpu_close(ctx);
         return PBGPU_EIO;
@@ -974,7 +994,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     K.blob = S.d_blob;
     K.jump = ctx->d_jump;
     K.lcg48 = ctx->d_lcg48;
-    K.counters = ctx->d_counters + 4 * seq_idx;
+    K.counters = ctx->d_counters + PB_CTR_WORDS * seq_idx;
     K.lds_pad = (uint32_t)env_int("PBGPU_LDS_PAD", (int)K.lds_pad);
     S.K = K;
     S.loaded = true;
@@ -1032,7 +1052,14 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
         (void)hipStreamSynchronize(ctx->land_stream);
     }
     if (f->reserved)
-        (void)hipEventDestroy((hipEvent_t)f->reserved);
+    {
+        frames_events *fe = (frames_events *)f->reserved;
+        if (fe->built)
+            (void)hipEventDestroy(fe->built);
+        if (fe->landed)
+            (void)hipEventDestroy(fe->landed);
+        delete fe;
+    }
     if (f->data)
         (void)hipFree(f->data);
     if (f->offsets)
@@ -1096,13 +1123,12 @@ static int mark_built(pbgpu_ctx *ctx, pbgpu_frames *out)
     // release between back-to-back builds that are never landed (bench)
     if (!ctx->land_events)
         return PBGPU_OK;
-    if (out->reserved == NULL)
-    {
-        hipEvent_t ev;
-        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        out->reserved = (void *)ev;
-    }
-    HIPCHK(hipEventRecord((hipEvent_t)out->reserved, ctx->stream));
+    frames_events *fe = frames_ev(out);
+    if (fe == NULL)
+        return PBGPU_ENOMEM;
+    if (fe->built == nullptr)
+        HIPCHK(hipEventCreateWithFlags(&fe->built, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(fe->built, ctx->stream));
     return PBGPU_OK;
 }
 
@@ -1123,6 +1149,13 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     if (((max_bytes + 15) & ~15ull) > out->capacity_bytes)
         return PBGPU_ENOSPC;
 
+    // a landing queued from this buffer must have read it before the build overwrites it
+    if (out->reserved && ((frames_events *)out->reserved)->land_pending)
+    {
+        frames_events *fe = (frames_events *)out->reserved;
+        HIPCHK(hipStreamWaitEvent(ctx->stream, fe->landed, 0));
+        fe->land_pending = false;
+    }
     pb_kargs K = S.K;
     K.first_iter = first_iter;
     K.n_frames = nf;
@@ -1432,8 +1465,9 @@ int pbgpu_copy_to_umem_async(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, 
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t ls = ctx->land_stream;
     ctx->land_events = true;
-    if (f->reserved)
-        HIPCHK(hipStreamWaitEvent(ls, (hipEvent_t)f->reserved, 0));
+    frames_events *fe = (frames_events *)f->reserved;
+    if (fe && fe->built)
+        HIPCHK(hipStreamWaitEvent(ls, fe->built, 0));
     else
         HIPCHK(hipStreamSynchronize(ctx->stream));
     uint8_t *dst = (uint8_t *)umem + (uint64_t)first_slot * slot_stride;
@@ -1495,6 +1529,14 @@ int pbgpu_copy_to_umem_async(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, 
         HIPCHK(hipEventCreateWithFlags(&op.ev, hipEventDisableTiming));
     HIPCHK(hipEventRecord(op.ev, ls));
     ctx->landings.push_back(op);
+    // the next pbgpu_build into this buffer waits for the landing (pbgpu.h)
+    frames_events *fw = frames_ev(const_cast<pbgpu_frames *>(f));
+    if (fw == NULL)
+        return PBGPU_ENOMEM;
+    if (fw->landed == nullptr)
+        HIPCHK(hipEventCreateWithFlags(&fw->landed, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(fw->landed, ls));
+    fw->land_pending = true;
     return PBGPU_OK;
 }
 
@@ -1512,19 +1554,26 @@ int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)
     if (ctx == NULL || n_seq < 0 || n_seq > PB_MAX_SEQUENCES)
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
-    std::vector<unsigned long long> h(4 * (size_t)PB_MAX_SEQUENCES);
+    if (n_seq == 0)
+        return PBGPU_OK;
+    // the kernels' per-workgroup adds land in PB_CTR_SHARDS shards per sequence: sum them
+    std::vector<unsigned long long> h(PB_CTR_WORDS * (size_t)n_seq);
     HIPCHK(hipMemcpyAsync(h.data(), ctx->d_counters, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    int bad = 0;
     for (int i = 0; i < n_seq; ++i)
     {
+        uint64_t p = 0, b = 0;
+        for (size_t k = 0; k < PB_CTR_SHARDS; ++k)
+        {
+            p += h[PB_CTR_WORDS * i + k * PB_CTR_STRIDE + 0];
+            b += h[PB_CTR_WORDS * i + k * PB_CTR_STRIDE + 1];
+        }
         if (pckts)
-            pckts[i] = h[4 * i + 0];
+            pckts[i] = p;
         if (bytes)
-            bytes[i] = h[4 * i + 1];
-        bad |= h[4 * i + 2] != 0;
+            bytes[i] = b;
     }
-    return bad ? PBGPU_EIO : PBGPU_OK;
+    return PBGPU_OK;
 }
 
 int pbgpu_set_timing(pbgpu_ctx *ctx, int mode)
@@ -1569,6 +1618,28 @@ int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches)
     ctx->pending.clear();
     if (ms_total)
         *ms_total = tot;
+    if (n_launches)
+        *n_launches = n;
+    return PBGPU_OK;
+}
+
+int pbgpu_kernel_times(pbgpu_ctx *ctx, double *ms_each, uint32_t cap, uint32_t *n_launches)
+{
+    if (ctx == NULL || (cap && ms_each == NULL))
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    uint32_t n = 0;
+    for (auto &p : ctx->pending)
+    {
+        HIPCHK(hipEventSynchronize(p.b));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+        if (n < cap)
+            ms_each[n] = ms;
+        ++n;
+        ctx->pool.push_back(p);
+    }
+    ctx->pending.clear();
     if (n_launches)
         *n_launches = n;
     return PBGPU_OK;

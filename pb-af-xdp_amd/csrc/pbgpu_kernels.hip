@@ -287,6 +287,17 @@ __device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg)
     return b < 8u * per ? (b & 7u) * per + (b >> 3) : b;
 }
 
+// The reference's total_pckts / total_bytes (sequence.c:633-642), counted as work is done:
+// each workgroup adds the frames it built and the bytes it stored (so a skipped store or a
+// short build shows in pbgpu_counters), into shard b % PB_CTR_SHARDS of its sequence — one
+// 128-B line per shard, so neighbouring workgroups' adds do not queue on one address.
+__device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t frames, uint64_t bytes)
+{
+    unsigned long long *c = K.counters + (uint64_t)(b % PB_CTR_SHARDS) * PB_CTR_STRIDE;
+    atomicAdd(c, (unsigned long long)frames);
+    atomicAdd(c + 1, (unsigned long long)bytes);
+}
+
 // ---------------- small fixed-length frames: one lane per frame ----------------
 //
 // Frames of <= 4*NDW bytes (configs[1] 64-B UDP, configs[3] 60-B TCP SYN, the
@@ -501,11 +512,8 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
         }
         pb_st16(out + 16 * c, v);
     }
-    if (blockIdx.x == 0 && tid == 0)
-    {
-        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
-        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
-    }
+    if (tid == 0)
+        pb_count(K, blockIdx.x, nfr, tile_bytes);
 }
 
 // XCD-owned form, for frame lengths that divide 4096 (64-B configs[1] frames,
@@ -573,10 +581,17 @@ __global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
             pb_st16(K.out + o, v);
         }
     }
-    if (b == 0 && tid == 0)
+    if (tid == 0)
     {
-        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
-        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+        // the stored pages: whole frames (flen = 4096 >> xs_fp_shift divides every page)
+        uint64_t by = 0;
+        for (uint32_t i = 0; i < np; ++i)
+        {
+            const uint32_t c = c0 + i * cs;
+            if (c < K.xs_nch)
+                by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
+        }
+        pb_count(K, b, by >> (12u - K.xs_fp_shift), by);
     }
 }
 
@@ -654,10 +669,21 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
             pb_st16(K.out + o, v);
         }
     }
-    if (b == 0 && tid == 0)
+    if (tid == 0)
     {
-        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
-        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+        // the stored pages, and the frames that start in them (each frame counted once)
+        uint64_t fr = 0, by = 0;
+        for (uint32_t i = 0; i < np; ++i)
+        {
+            const uint32_t c = c0 + i * cs;
+            if (c >= K.xs_nch)
+                continue;
+            const uint64_t p0 = (uint64_t)c * PB_XPG;
+            by += min((uint64_t)PB_XPG, T - p0);
+            const uint64_t fa = (p0 + flen - 1) / flen, fb = min(K.n_frames, (p0 + PB_XPG + flen - 1) / flen);
+            fr += fb > fa ? fb - fa : 0;
+        }
+        pb_count(K, b, fr, by);
     }
 }
 
@@ -957,10 +983,12 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
             }
         }
     }
-    if (K.fixed_len && blockIdx.x == 0 && tid == 0)
+    if (tid == 0 && nfr)
     {
-        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
-        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
+        // every byte of the workgroup's frames is stored by exactly one of its lanes
+        const uint64_t b0 = ((uint64_t)s_bhi[0] << 32) | s_blo[0];
+        const uint64_t b1 = (((uint64_t)s_bhi[nfr - 1] << 32) | s_blo[nfr - 1]) + s_flen[nfr - 1];
+        pb_count(K, blockIdx.x, nfr, b1 - b0);
     }
 }
 
@@ -1262,11 +1290,8 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
         PB_LAP(4, tlap);
     }
     PB_STAMP(6);
-    if (K.fixed_len && blockIdx.x == 0 && tid == 0)
-    {
-        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
-        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
-    }
+    if (tid == 0 && nfr) // the windows stored the workgroup's frames' bytes, each once
+        pb_count(K, blockIdx.x, nfr, s_r[nfr - 1] + s_len[nfr - 1] - s_r[0]);
 }
 
 // ---------------- fixed-length staged: pb_fstage_kernel ----------------
@@ -1477,11 +1502,8 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
         PB_LAP(4, tt);
     }
     PB_STAMP(6);
-    if (blockIdx.x == 0 && tid == 0)
-    {
-        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
-        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
-    }
+    if (tid == 0) // (PBGPU_FST_DBG bit 1 skips the stores: nothing stored, nothing counted)
+        pb_count(K, blockIdx.x, nfr, (K.fst_dbg & 2u) ? 0ull : (uint64_t)nfr * flen);
 }
 
 // ---------------- any length, every payload random: pb_vstage_kernel ----------------
@@ -1969,11 +1991,8 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         PB_LAP(4, tt);
     }
     PB_STAMP(6);
-    if (K.fixed_len && bxr == 0 && tid == 0)
-    {
-        atomicAdd(K.counters + 0, (unsigned long long)K.n_frames);
-        atomicAdd(K.counters + 1, (unsigned long long)K.total_bytes);
-    }
+    if (tid == 0) // the workgroup stores exactly [lo, hi) (PBGPU_FST_DBG bit 1: the stores are skipped)
+        pb_count(K, bxr, nown, (K.fst_dbg & 2u) ? 0ull : hi_abs - lo_abs);
 }
 
 // ---------------- variable length: lengths -> offsets -> tile map ----------------
@@ -2003,8 +2022,7 @@ __global__ __launch_bounds__(256) void pb_len_reduce(pb_kargs K, unsigned long l
 
 // single workgroup: exclusive scan of the block sums in place
 __global__ __launch_bounds__(1024) void pb_scan_blocks(unsigned long long *block_sums, uint32_t nblocks,
-                                                       uint64_t *offsets, uint64_t n_frames,
-                                                       unsigned long long *counters)
+                                                       uint64_t *offsets, uint64_t n_frames)
 {
     __shared__ unsigned long long s_v[1024];
     unsigned long long carry = 0;
@@ -2028,11 +2046,7 @@ __global__ __launch_bounds__(1024) void pb_scan_blocks(unsigned long long *block
         carry += tot;
     }
     if (threadIdx.x == 0)
-    {
-        offsets[n_frames] = carry;
-        atomicAdd(counters + 0, (unsigned long long)n_frames);
-        atomicAdd(counters + 1, carry);
-    }
+        offsets[n_frames] = carry; // (the build kernels count frames and bytes as they store them)
 }
 
 __global__ __launch_bounds__(256) void pb_len_scan(pb_kargs K, const unsigned long long *block_sums,
@@ -2364,7 +2378,7 @@ extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t *bsum, 
                                              uint32_t n_l2, uint64_t *offsets, hipStream_t st)
 {
     hipLaunchKernelGGL(pb_len_wgsum, dim3(n_l2), dim3(256), 0, st, *K, K->stage_wgf, nblk, bsum, l2);
-    hipLaunchKernelGGL(pb_scan_blocks, dim3(1), dim3(1024), 0, st, l2, n_l2, offsets, K->n_frames, K->counters);
+    hipLaunchKernelGGL(pb_scan_blocks, dim3(1), dim3(1024), 0, st, l2, n_l2, offsets, K->n_frames);
     return hipGetLastError();
 }
 
@@ -2372,8 +2386,7 @@ extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *
                                          uint64_t *offsets, hipStream_t st)
 {
     hipLaunchKernelGGL(pb_len_reduce, dim3(nblocks), dim3(256), 0, st, *K, block_sums);
-    hipLaunchKernelGGL(pb_scan_blocks, dim3(1), dim3(1024), 0, st, block_sums, nblocks, offsets, K->n_frames,
-                       K->counters);
+    hipLaunchKernelGGL(pb_scan_blocks, dim3(1), dim3(1024), 0, st, block_sums, nblocks, offsets, K->n_frames);
     hipLaunchKernelGGL(pb_len_scan, dim3(nblocks), dim3(256), 0, st, *K, (const unsigned long long *)block_sums,
                        offsets);
     return hipGetLastError();

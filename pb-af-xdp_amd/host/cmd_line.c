@@ -5,10 +5,16 @@
  * through atoi (src/cmd_line.c:24-69); unknown options are skipped silently
  * (main.c sets opterr = 0 before the passes).
  */
+#define _GNU_SOURCE
 #include "cmd_line.h"
 
+#include <errno.h>
 #include <getopt.h>
+#include <linux/if_xdp.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <sys/random.h>
+#include <time.h>
 
 enum
 {
@@ -27,6 +33,7 @@ enum
     OPT_SINGLEFOLD,
     OPT_PCAP,
     OPT_TX,
+    OPT_VERYRANDOM,
 };
 
 static const struct option af_xdp_opts[] = {
@@ -45,6 +52,7 @@ static const struct option af_xdp_opts[] = {
     {"singlefold", no_argument, NULL, OPT_SINGLEFOLD},
     {"pcap", required_argument, NULL, OPT_PCAP},
     {"tx", required_argument, NULL, OPT_TX},
+    {"veryrandom", no_argument, NULL, OPT_VERYRANDOM},
     {NULL, 0, NULL, 0},
 };
 
@@ -76,6 +84,7 @@ void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *c, int argc, char **argv)
             break;
         case OPT_BATCHSIZE:
             c->batch_size = (unsigned short)atoi(optarg);
+            c->batch_set = 1;
             break;
         case OPT_SKB:
             c->skb_mode = 1;
@@ -97,6 +106,7 @@ void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *c, int argc, char **argv)
             break;
         case OPT_SEED:
             c->seed_base = strtoull(optarg, NULL, 0);
+            c->seed_set = 1;
             break;
         case OPT_LITERAL:
             c->literal_payload = 1;
@@ -110,8 +120,69 @@ void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *c, int argc, char **argv)
         case OPT_TX:
             c->tx = optarg;
             break;
+        case OPT_VERYRANDOM:
+            c->very_random = 1;
+            break;
         default:
             break;
         }
     }
+}
+
+int pb_af_xdp_setup(const struct cmd_line_af_xdp *c, int verbose)
+{
+    if (c->skb_mode && c->zero_copy)
+    {
+        fprintf(stderr, "--skb and --zerocopy cannot be combined: SKB (generic XDP) mode sends in copy mode.\n");
+        return -EINVAL;
+    }
+    if (c->batch_set && c->batch_size == 0)
+    {
+        fprintf(stderr, "--batchsize must be at least 1.\n");
+        return -EINVAL;
+    }
+    if (!verbose)
+        return 0;
+    /* af_xdp.c:291-364, line for line */
+    if (c->zero_copy)
+        fprintf(stdout, "Running AF_XDP sockets in zero-copy mode.\n");
+    else if (c->copy)
+        fprintf(stdout, "Running AF_XDP sockets in copy mode.\n");
+    if (c->no_wake_up)
+        fprintf(stdout, "Running AF_XDP sockets in no wake-up mode.\n");
+    if (c->queue_set)
+        fprintf(stdout, "Running AF_XDP sockets with one queue ID => %d.\n", c->queue);
+    if (c->shared_umem)
+        fprintf(stdout, "Running AF_XDP sockets with shared UMEM mode.\n");
+    if (c->skb_mode)
+        fprintf(stdout, "Running AF_XDP sockets in SKB mode.\n");
+    fprintf(stdout, "Running AF_XDP sockets with batch size => %d.\n", c->batch_size);
+    return 0;
+}
+
+uint16_t pb_bind_flags(const struct cmd_line_af_xdp *c)
+{
+    uint16_t bf = c->no_wake_up ? 0 : XDP_USE_NEED_WAKEUP;
+    if (c->zero_copy)
+        bf |= XDP_ZEROCOPY;
+    else if (c->copy || c->skb_mode) /* generic (SKB) XDP has no zero-copy path */
+        bf |= XDP_COPY;
+    return bf;
+}
+
+uint64_t pb_resolve_seed(struct cmd_line_af_xdp *c)
+{
+    if (c->seed_set)
+        return c->seed_base;
+    uint64_t s = 0;
+    if (c->very_random && getrandom(&s, sizeof s, 0) == (ssize_t)sizeof s)
+    {
+        c->seed_base = s;
+        return s;
+    }
+    struct timespec ts;
+    clock_gettime(CLOCK_BOOTTIME, &ts);
+    s = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+    c->seed_base = s;
+    return s;
 }

@@ -32,7 +32,23 @@ typedef struct cmd_line_af_xdp
     int single_fold;     /* --singlefold: one-fold IPv4 checksum (quirk B6) */
     const char *pcap;    /* --pcap FILE: write built frames to a pcap file */
     const char *tx;      /* --tx xsk: AF_XDP sockets; otherwise the in-memory TX ring (xsk_ring.h) */
+    int seed_set;        /* --seed given; otherwise pb_resolve_seed() draws seed_base per run */
+    int very_random;     /* --veryrandom: draw it with getrandom() (VERY_RANDOM, sequence.h:36) */
+    int batch_set;       /* --batchsize given: TX descriptors per reserve / submit (else one landed chunk) */
 } cmd_line_af_xdp_t;
 
 void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *cmd_af_xdp, int argc, char **argv);
 void cmd_line_af_xdp_defaults(struct cmd_line_af_xdp *cmd_af_xdp);
+
+/* setup_af_xdp_variables() (af_xdp.c:289-365): the reference's verbose lines, and the
+ * checks this build adds: --skb (SKB / generic XDP mode, xdp_flags = XDP_FLAGS_SKB_MODE)
+ * runs the socket in copy mode, so --skb with --zerocopy is refused; --batchsize 0 is
+ * refused.  Returns 0, or -EINVAL after a message on stderr. */
+int pb_af_xdp_setup(const struct cmd_line_af_xdp *cmd_af_xdp, int verbose);
+/* bind flags of a socket (af_xdp.c:291-320): need-wakeup unless --nowakeup;
+ * --zerocopy, else --copy or --skb -> XDP_COPY */
+uint16_t pb_bind_flags(const struct cmd_line_af_xdp *cmd_af_xdp);
+/* The seed stream's base: --seed S as given; otherwise drawn once per run, as the
+ * reference draws each iteration's seed (sequence.c:434-441): CLOCK_BOOTTIME
+ * nanoseconds, or getrandom() with --veryrandom.  Stores it in seed_base. */
+uint64_t pb_resolve_seed(struct cmd_line_af_xdp *cmd_af_xdp);

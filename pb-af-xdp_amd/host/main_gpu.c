@@ -79,7 +79,7 @@ static const struct option common_opts[] = {
     {"gpu", required_argument, NULL, O_SECOND_PASS}, {"gpubatch", required_argument, NULL, O_SECOND_PASS},
     {"seed", required_argument, NULL, O_SECOND_PASS}, {"literal", no_argument, NULL, O_SECOND_PASS},
     {"singlefold", no_argument, NULL, O_SECOND_PASS}, {"pcap", required_argument, NULL, O_SECOND_PASS},
-    {"tx", required_argument, NULL, O_SECOND_PASS},
+    {"tx", required_argument, NULL, O_SECOND_PASS}, {"veryrandom", no_argument, NULL, O_SECOND_PASS},
     {NULL, 0, NULL, 0},
 };
 
@@ -176,7 +176,7 @@ static void print_cmd_help(void)
                     "-h --help => Print out help menu and exit program.\n"
                     "-z --cli => Enables the first sequence/packet override (README.md first-sequence options).\n\n"
                     "AF_XDP: --queue --nowakeup --sharedumem --batchsize --skb --zerocopy --copy\n"
-                    "GPU: --gpus N --gpu I --gpubatch K --seed S --literal --singlefold --pcap FILE --tx xsk\n");
+                    "GPU: --gpus N --gpu I --gpubatch K --seed S --veryrandom --literal --singlefold --pcap FILE --tx xsk\n");
 }
 
 int main(int argc, char **argv)
@@ -212,6 +212,11 @@ int main(int argc, char **argv)
     optind = 0; /* main.c:45 */
     parse_cmd_line_af_xdp(&cmd_af_xdp, argc, argv);
     pb_set_verbose(cmd.verbose);
+    if (pb_af_xdp_setup(&cmd_af_xdp, cmd.verbose) != 0) /* setup_af_xdp_variables (main.c:49) */
+        return EXIT_FAILURE;
+    /* the seed stream's base: --seed, else drawn from CLOCK_BOOTTIME (or getrandom with
+     * --veryrandom) the way the reference seeds every iteration (sequence.c:434-441) */
+    pb_resolve_seed(&cmd_af_xdp);
 
     if (cmd.config == NULL) /* main.c:51-61 */
     {
@@ -251,6 +256,21 @@ int main(int argc, char **argv)
                     cfg->seq[i].ip.dst_ip ? cfg->seq[i].ip.dst_ip : "(none)",
                     cfg->seq[i].ip.protocol ? cfg->seq[i].ip.protocol : "udp", cfg->seq[i].pl_cnt);
         return EXIT_SUCCESS;
+    }
+    fprintf(stdout, "Seed base => 0x%016llx (%s; replay with --seed 0x%llx).\n", (unsigned long long)cmd_af_xdp.seed_base,
+            cmd_af_xdp.seed_set ? "--seed" : (cmd_af_xdp.very_random ? "getrandom" : "CLOCK_BOOTTIME"),
+            (unsigned long long)cmd_af_xdp.seed_base);
+    for (int i = 0; i < seq_cnt && cmd_af_xdp.literal_payload; ++i)
+    {
+        int random = 0;
+        for (int j = 0; j < cfg->seq[i].pl_cnt; ++j)
+            random |= cfg->seq[i].pls[j].exact == NULL && !cfg->seq[i].pls[j].is_static && cfg->seq[i].pls[j].max_len > 0;
+        if (cfg->seq[i].pl_cnt > 1 && random)
+            fprintf(stderr,
+                    "[%d] WARNING - --literal with several payloads follows the declared rule: the shadowed loop "
+                    "(sequence.c:552) reads the other payloads' setup lengths, where the reference reads the previous "
+                    "iteration's (quirk B8).\n",
+                    i + 1);
     }
     pb_pcap_t *pcap = NULL;
     if (cmd_af_xdp.pcap)

@@ -35,6 +35,7 @@ static uint64_t total_pckts[PB_MAX_SEQUENCES];
 static uint64_t total_bytes[PB_MAX_SEQUENCES];
 static uint64_t claimed_frames[PB_MAX_SEQUENCES]; /* max_pckts quota handed to workers */
 static uint64_t tx_descs[PB_MAX_SEQUENCES], tx_comps[PB_MAX_SEQUENCES], tx_wakeups[PB_MAX_SEQUENCES];
+static uint64_t umem_allocs[PB_MAX_SEQUENCES]; /* UMEMs allocated per sequence (--sharedumem: one) */
 static time_t start_time[PB_MAX_SEQUENCES];
 static time_t end_time[PB_MAX_SEQUENCES];
 static uint16_t seq_cnt;
@@ -81,6 +82,15 @@ int pb_sequence_totals(uint16_t seq, uint64_t *pckts, uint64_t *bytes)
         *pckts = __atomic_load_n(&total_pckts[seq], __ATOMIC_RELAXED);
     if (bytes)
         *bytes = __atomic_load_n(&total_bytes[seq], __ATOMIC_RELAXED);
+    return PBGPU_OK;
+}
+
+int pb_sequence_umems(uint16_t seq, uint64_t *umems)
+{
+    if (seq >= PB_MAX_SEQUENCES)
+        return PBGPU_EINVAL;
+    if (umems)
+        *umems = __atomic_load_n(&umem_allocs[seq], __ATOMIC_RELAXED);
     return PBGPU_OK;
 }
 
@@ -166,6 +176,20 @@ void pb_set_builder(const pb_builder_t *b)
 
 /* ---------------- worker ---------------- */
 
+/* --sharedumem (af_xdp.c:412-428): one UMEM of NUM_FRAMES slots per sequence, shared by its
+ * threads; thread t owns the slot range [t * slots, (t + 1) * slots) (the reference's threads
+ * all write the same frame indices, B10).  With AF_XDP sockets thread 0's socket registers it
+ * and the others bind with XDP_SHARED_UMEM to that socket's fd. */
+typedef struct shared_umem
+{
+    uint8_t *base;
+    uint32_t slots; /* per thread, a power of two */
+    int refs;       /* workers still using it; the last one frees it */
+    int fd;         /* thread 0's socket, once open (-1 before; -2 if it failed) */
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+} shared_umem_t;
+
 typedef struct worker_arg
 {
     pb_sequence_t seq;
@@ -175,7 +199,22 @@ typedef struct worker_arg
     int shard;   /* TX thread index = queue id (af_xdp.c:443) */
     int n_shards;
     struct cmd_line_af_xdp cmd;
+    shared_umem_t *shared; /* --sharedumem, else NULL */
 } worker_arg_t;
+
+static void shared_release(shared_umem_t *u)
+{
+    pthread_mutex_lock(&u->mu);
+    const int last = --u->refs == 0;
+    pthread_mutex_unlock(&u->mu);
+    if (last)
+    {
+        pthread_mutex_destroy(&u->mu);
+        pthread_cond_destroy(&u->cv);
+        free(u->base);
+        free(u);
+    }
+}
 
 static double now_s(void)
 {
@@ -250,7 +289,10 @@ static void *gpu_worker(void *p)
     memset(&xsk, 0, sizeof xsk);
     xsk.fd = -1;
     sink_arg_t sink = {w->shard, seq_num};
-    const size_t umem_bytes = (size_t)PB_NUM_FRAMES * PB_FRAME_SIZE;
+    /* this thread's UMEM slots: its own NUM_FRAMES, or its range of the sequence's shared UMEM */
+    const uint32_t nslots = w->shared ? w->shared->slots : PB_NUM_FRAMES;
+    const uint32_t slot_base = w->shared ? (uint32_t)w->shard * nslots : 0;
+    const size_t umem_bytes = (size_t)nslots * PB_FRAME_SIZE;
     uint16_t lens[PB_NUM_FRAMES];
     int rc;
 
@@ -324,42 +366,79 @@ static void *gpu_worker(void *p)
         last_error = rc;
         goto out;
     }
-    if (posix_memalign((void **)&umem, (size_t)sysconf(_SC_PAGESIZE), umem_bytes) != 0)
+    uint8_t *umem_base = NULL; /* the UMEM the TX ring addresses (shared: the sequence's) */
+    if (w->shared)
     {
-        umem = NULL;
-        last_error = PBGPU_ENOMEM;
-        goto out;
+        umem_base = w->shared->base;
+        umem = umem_base + (size_t)slot_base * PB_FRAME_SIZE;
     }
-    memset(umem, 0, umem_bytes);
+    else
+    {
+        if (posix_memalign((void **)&umem, (size_t)sysconf(_SC_PAGESIZE), umem_bytes) != 0)
+        {
+            umem = NULL;
+            last_error = PBGPU_ENOMEM;
+            goto out;
+        }
+        memset(umem, 0, umem_bytes);
+        umem_base = umem;
+        __atomic_add_fetch(&umem_allocs[w->seq_idx], 1, __ATOMIC_RELAXED);
+    }
     registered = B->host_register(ctx, umem, umem_bytes) == 0;
 
     /* the TX queue: an AF_XDP socket on queue `shard` (or --queue, af_xdp.c:443),
      * or the in-memory loopback whose consumer hands frames to the TX hook */
     if (w->cmd.tx && strcmp(w->cmd.tx, "xsk") == 0)
     {
-        uint16_t bf = w->cmd.no_wake_up ? 0 : XDP_USE_NEED_WAKEUP;
-        if (w->cmd.zero_copy)
-            bf |= XDP_ZEROCOPY;
-        else if (w->cmd.copy)
-            bf |= XDP_COPY;
+        const uint16_t bf = pb_bind_flags(&w->cmd);
         const uint32_t q = w->cmd.queue_set ? (uint32_t)w->cmd.queue : (uint32_t)w->shard;
-        if ((rc = pb_xsk_open(&xsk, w->device, q, umem, PB_NUM_FRAMES, PB_FRAME_SIZE, bf)) != 0)
+        int shared_fd = -1;
+        if (w->shared && w->shard > 0)
+        {
+            /* thread 0's socket owns the shared UMEM registration: wait for it */
+            pthread_mutex_lock(&w->shared->mu);
+            while (w->shared->fd == -1 && !stop_requested)
+                pthread_cond_wait(&w->shared->cv, &w->shared->mu);
+            shared_fd = w->shared->fd;
+            pthread_mutex_unlock(&w->shared->mu);
+            if (shared_fd < 0)
+            {
+                last_error = PBGPU_EIO;
+                goto out;
+            }
+        }
+        rc = pb_xsk_open(&xsk, w->device, q, umem_base, nslots, PB_FRAME_SIZE, bf, shared_fd, slot_base,
+                         w->shared ? (uint32_t)PB_NUM_FRAMES : nslots);
+        if (w->shared && w->shard == 0)
+        {
+            pthread_mutex_lock(&w->shared->mu);
+            w->shared->fd = rc == 0 ? xsk.fd : -2;
+            pthread_cond_broadcast(&w->shared->cv);
+            pthread_mutex_unlock(&w->shared->mu);
+        }
+        if (rc != 0)
         {
             fprintf(stderr, "Could not setup AF_XDP socket at index %d :: %s (%d).\n", w->shard, strerror(-rc), -rc);
             last_error = rc;
             goto out;
         }
     }
-    else if ((rc = pb_xsk_loopback(&xsk, umem, PB_NUM_FRAMES, PB_FRAME_SIZE)) != 0)
+    else if ((rc = pb_xsk_loopback(&xsk, umem_base, nslots, PB_FRAME_SIZE)) != 0)
     {
         last_error = rc;
         goto out;
     }
     else
     {
+        xsk.slot_base = slot_base;
         xsk.loop_sink = tx_hook ? tx_sink : NULL;
         xsk.loop_ctx = &sink;
+        const char *hold = getenv("PB_LOOP_HOLD"); /* tests: frames the loopback keeps in flight */
+        xsk.loop_hold = hold ? (uint32_t)atoi(hold) : 0u;
     }
+    /* --batchsize: descriptors per reserve / submit / complete (send_packet, af_xdp.c:184-233);
+     * without it one landed chunk is one submit */
+    xsk.batch = w->cmd.batch_set ? w->cmd.batch_size : 0u;
 
     const double t0 = now_s();
     uint64_t my_frames = 0; /* this thread's frames: the delay pacing (per thread) */
@@ -402,7 +481,7 @@ static void *gpu_worker(void *p)
                 {
                     if (qn)
                         break;
-                    if (pb_xsk_complete(&xsk, PB_NUM_FRAMES) == 0)
+                    if (pb_xsk_complete(&xsk, nslots) == 0)
                         sched_yield();
                     if (stop_requested)
                         break;
@@ -411,8 +490,8 @@ static void *gpu_worker(void *p)
                 uint32_t n = free_slots < PB_LAND_CHUNK ? free_slots : PB_LAND_CHUNK;
                 if ((uint64_t)n > nf - f_issue)
                     n = (uint32_t)(nf - f_issue);
-                if (n > PB_NUM_FRAMES - land_slot) /* the slot ring wraps: a chunk never does */
-                    n = PB_NUM_FRAMES - land_slot;
+                if (n > nslots - land_slot) /* the slot ring wraps: a chunk never does */
+                    n = nslots - land_slot;
                 if ((rc = B->land(ctx, fr[cur], umem, PB_FRAME_SIZE, land_slot, f_issue, n, lens + land_slot)) != 0)
                 {
                     fprintf(stderr, "[%d] Error landing frames from GPU %d :: %s.\n", seq_num, w->gpu,
@@ -424,7 +503,7 @@ static void *gpu_worker(void *p)
                 qn_[(qh + qn) % PB_LAND_INFLIGHT] = n;
                 ++qn;
                 in_land += n;
-                land_slot = (land_slot + n) & (PB_NUM_FRAMES - 1);
+                land_slot = (land_slot + n) & (nslots - 1);
                 f_issue += n;
             }
             if (done || qn == 0)
@@ -461,6 +540,11 @@ static void *gpu_worker(void *p)
                     if (__atomic_compare_exchange_n(&total_bytes[w->seq_idx], &tot, tot + b, 0, __ATOMIC_RELAXED,
                                                     __ATOMIC_RELAXED))
                     {
+                        /* the budget ends inside this chunk: its remaining frames are never sent, so
+                         * no further landing may be queued — the slot accounting above (in_land,
+                         * land_slot) assumed the whole chunk would go out */
+                        if (m < n)
+                            done = 1;
                         n = m, bytes = b;
                         break;
                     }
@@ -533,21 +617,34 @@ static void *gpu_worker(void *p)
         ++step;
     }
     /* drain: every submitted frame completes before the UMEM goes away */
+    xsk.loop_hold = 0;
     for (int spin = 0; xsk.outstanding_tx && spin < 100000; ++spin)
-        if (pb_xsk_complete(&xsk, PB_NUM_FRAMES) == 0)
+        if (pb_xsk_complete(&xsk, nslots) == 0)
             sched_yield();
 out:
     end_time[w->seq_idx] = time(NULL);
     __atomic_add_fetch(&tx_descs[w->seq_idx], xsk.completed + xsk.outstanding_tx, __ATOMIC_RELAXED);
     __atomic_add_fetch(&tx_comps[w->seq_idx], xsk.completed, __ATOMIC_RELAXED);
     __atomic_add_fetch(&tx_wakeups[w->seq_idx], xsk.wakeups, __ATOMIC_RELAXED);
+    if (w->shared && w->shard == 0 && xsk.fd < 0 && w->cmd.tx && strcmp(w->cmd.tx, "xsk") == 0)
+    {
+        /* thread 0 failed before publishing its socket: release the waiting threads */
+        pthread_mutex_lock(&w->shared->mu);
+        if (w->shared->fd == -1)
+            w->shared->fd = -2;
+        pthread_cond_broadcast(&w->shared->cv);
+        pthread_mutex_unlock(&w->shared->mu);
+    }
     pb_xsk_close(&xsk);
     if (umem)
     {
         if (registered)
             B->host_unregister(ctx, umem);
-        free(umem);
+        if (!w->shared)
+            free(umem);
     }
+    if (w->shared)
+        shared_release(w->shared);
     for (int i = 0; i < 2; ++i)
         if (fr[i])
             B->free_frames(ctx, fr[i]);
@@ -578,6 +675,38 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
     if (t_cnt > PB_MAX_WORKERS - worker_cnt)
         t_cnt = PB_MAX_WORKERS - worker_cnt;
     start_time[idx] = time(NULL);
+    shared_umem_t *shared = NULL;
+    if (cmd.shared_umem && t_cnt > 0)
+    {
+        /* one UMEM for the sequence's threads (af_xdp.c:412-428), each its own power-of-two
+         * slot range */
+        uint32_t slots = PB_NUM_FRAMES;
+        while (slots > 1 && slots * (uint32_t)t_cnt > PB_NUM_FRAMES)
+            slots >>= 1;
+        if (slots * (uint32_t)t_cnt > PB_NUM_FRAMES)
+        {
+            fprintf(stderr, "[%d] Too many threads (%d) for one shared UMEM of %d frames.\n", idx + 1, t_cnt,
+                    PB_NUM_FRAMES);
+            last_error = PBGPU_EINVAL;
+            return;
+        }
+        shared = (shared_umem_t *)calloc(1, sizeof *shared);
+        if (shared == NULL ||
+            posix_memalign((void **)&shared->base, (size_t)sysconf(_SC_PAGESIZE),
+                           (size_t)PB_NUM_FRAMES * PB_FRAME_SIZE) != 0)
+        {
+            free(shared);
+            last_error = PBGPU_ENOMEM;
+            return;
+        }
+        memset(shared->base, 0, (size_t)PB_NUM_FRAMES * PB_FRAME_SIZE);
+        shared->slots = slots;
+        shared->fd = -1;
+        shared->refs = 1; /* seq_send's own reference, dropped after the threads are started */
+        pthread_mutex_init(&shared->mu, NULL);
+        pthread_cond_init(&shared->cv, NULL);
+        __atomic_add_fetch(&umem_allocs[idx], 1, __ATOMIC_RELAXED);
+    }
     const int old = worker_cnt;
     for (int t = 0; t < t_cnt; ++t)
     {
@@ -591,13 +720,31 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
         w->shard = t;
         w->n_shards = t_cnt;
         w->cmd = cmd;
+        w->shared = shared;
+        if (shared)
+        {
+            pthread_mutex_lock(&shared->mu);
+            ++shared->refs;
+            pthread_mutex_unlock(&shared->mu);
+        }
         if (pthread_create(&workers[worker_cnt], NULL, gpu_worker, w) != 0)
         {
+            if (shared)
+                shared_release(shared);
             free(w);
             break;
         }
         joined[worker_cnt] = 0;
         ++worker_cnt;
+    }
+    if (shared)
+    {
+        pthread_mutex_lock(&shared->mu);
+        if (worker_cnt == old) /* no thread started: nobody will publish a socket */
+            shared->fd = -2;
+        pthread_cond_broadcast(&shared->cv);
+        pthread_mutex_unlock(&shared->mu);
+        shared_release(shared);
     }
     if (seq.block || seq_cnt >= seqc - 1) /* sequence.c:765, including its off-by-one (B10) */
         for (int i = old; i < worker_cnt; ++i)
@@ -661,6 +808,7 @@ void pb_reset(void)
     memset(tx_descs, 0, sizeof tx_descs);
     memset(tx_comps, 0, sizeof tx_comps);
     memset(tx_wakeups, 0, sizeof tx_wakeups);
+    memset(umem_allocs, 0, sizeof umem_allocs);
     memset(start_time, 0, sizeof start_time);
     memset(end_time, 0, sizeof end_time);
     stop_requested = 0;

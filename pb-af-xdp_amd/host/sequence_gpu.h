@@ -5,7 +5,8 @@
  * seq_send() starts the sequence's TX threads — `threads` of them as in the
  * reference (sequence.c:741; 0 = one per GPU here, where the reference takes
  * get_nprocs()), spread round robin over --gpus GPUs.  Thread t owns a UMEM of
- * NUM_FRAMES x FRAME_SIZE slots (af_xdp.h:23-24), a TX ring + completion ring
+ * NUM_FRAMES x FRAME_SIZE slots (af_xdp.h:23-24; with --sharedumem its own
+ * power-of-two slot range of one UMEM per sequence), a TX ring + completion ring
  * (an AF_XDP socket on queue t, or the in-memory loopback), and shard t of the
  * iteration space.  It builds batches of iterations with pbgpu_build() into two
  * device buffers alternately — batch n + 1 builds on the GPU while batch n is
@@ -58,6 +59,8 @@ void pb_reset(void);
 /* TX descriptor / wakeup / completion counts summed over the finished workers
  * of a sequence (the ring protocol's own accounting). */
 int pb_sequence_tx_stats(uint16_t seq, uint64_t *descs, uint64_t *completions, uint64_t *wakeups);
+/* UMEMs allocated for a sequence: one per thread, or one in all with --sharedumem. */
+int pb_sequence_umems(uint16_t seq, uint64_t *umems);
 
 /* ---- the frame builder behind the workers ----
  * Default: libpbgpu (pbgpu_open / _load_sequence / _build / _copy_to_umem).

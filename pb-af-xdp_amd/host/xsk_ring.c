@@ -199,12 +199,14 @@ static int map_ring(int fd, pb_xsk_ring_t *r, const struct xdp_ring_offset *off,
 }
 
 int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, uint32_t n_frames,
-                uint32_t frame_size, uint16_t bind_flags)
+                uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames)
 {
-    if (x == NULL || ifname == NULL || umem == NULL || n_frames == 0 || (n_frames & (n_frames - 1)))
+    if (x == NULL || ifname == NULL || umem == NULL || n_frames == 0 || (n_frames & (n_frames - 1)) ||
+        slot_base + n_frames > (umem_frames ? umem_frames : n_frames))
         return -EINVAL;
     memset(x, 0, sizeof *x);
     x->fd = -1;
+    x->slot_base = slot_base;
     const unsigned ifindex = if_nametoindex(ifname);
     if (ifindex == 0)
         return -ENODEV;
@@ -215,15 +217,16 @@ int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, 
     x->umem = umem;
     x->n_frames = n_frames;
     x->frame_size = frame_size;
-    /* xsk_umem__create: register the UMEM, size the fill and completion rings */
+    /* xsk_umem__create: register the UMEM (once: a shared UMEM stays registered on the
+     * first socket), size this socket's fill and completion rings */
     struct xdp_umem_reg mr;
     memset(&mr, 0, sizeof mr);
     mr.addr = (uint64_t)(uintptr_t)umem;
-    mr.len = (uint64_t)n_frames * frame_size;
+    mr.len = (uint64_t)(umem_frames ? umem_frames : n_frames) * frame_size;
     mr.chunk_size = frame_size;
     int rc = 0;
     const int ring_n = (int)n_frames;
-    if (setsockopt(fd, SOL_XDP, XDP_UMEM_REG, &mr, sizeof mr) ||
+    if ((shared_fd < 0 && setsockopt(fd, SOL_XDP, XDP_UMEM_REG, &mr, sizeof mr)) ||
         setsockopt(fd, SOL_XDP, XDP_UMEM_FILL_RING, &ring_n, sizeof ring_n) ||
         setsockopt(fd, SOL_XDP, XDP_UMEM_COMPLETION_RING, &ring_n, sizeof ring_n) ||
         /* xsk_socket__create with a TX ring only (af_xdp.c:103-165) */
@@ -252,6 +255,11 @@ int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, 
     sxdp.sxdp_ifindex = ifindex;
     sxdp.sxdp_queue_id = queue;
     sxdp.sxdp_flags = bind_flags;
+    if (shared_fd >= 0)
+    {
+        sxdp.sxdp_flags = XDP_SHARED_UMEM; /* the kernel takes the copy / wakeup mode of the UMEM's owner */
+        sxdp.sxdp_shared_umem_fd = (uint32_t)shared_fd;
+    }
     if (bind(fd, (struct sockaddr *)&sxdp, sizeof sxdp))
     {
         rc = -errno;
@@ -291,7 +299,11 @@ uint32_t pb_xsk_complete(pb_xsk_t *x, uint32_t max)
         if (x->fd >= 0)
             (void)sendto(x->fd, NULL, 0, MSG_DONTWAIT, NULL, 0);
         else if (x->loop_auto)
-            (void)pb_xsk_loop_consume(x, x->n_frames, x->loop_sink, x->loop_ctx);
+        {
+            const uint32_t pending = __atomic_load_n(x->tx.producer, __ATOMIC_ACQUIRE) - *x->tx.consumer;
+            if (pending > x->loop_hold)
+                (void)pb_xsk_loop_consume(x, pending - x->loop_hold, x->loop_sink, x->loop_ctx);
+        }
     }
     uint32_t idx = 0;
     const uint32_t n = pb_ring_cons_peek(&x->cq, max, &idx);
@@ -315,27 +327,33 @@ int pb_xsk_send(pb_xsk_t *x, const uint16_t *lens, uint32_t n)
         return 0;
     if (n > pb_xsk_free_slots(x))
         return -ENOSPC;
-    uint32_t idx = 0;
-    /* af_xdp.c:184-190: reap completions until the TX ring has room */
-    for (uint64_t spin = 0; pb_ring_prod_reserve(&x->tx, n, &idx) < n; ++spin)
+    const uint32_t bs = x->batch ? x->batch : n;
+    for (uint32_t sent = 0; sent < n;)
     {
-        if (pb_xsk_complete(x, x->n_frames) == 0 && spin > 1000)
-            sched_yield();
-        if (spin > (1ull << 26))
-            return -EAGAIN;
+        const uint32_t k = n - sent < bs ? n - sent : bs;
+        uint32_t idx = 0;
+        /* af_xdp.c:184-190: reap completions until the TX ring has room */
+        for (uint64_t spin = 0; pb_ring_prod_reserve(&x->tx, k, &idx) < k; ++spin)
+        {
+            if (pb_xsk_complete(x, x->n_frames) == 0 && spin > 1000)
+                sched_yield();
+            if (spin > (1ull << 26))
+                return -EAGAIN;
+        }
+        for (uint32_t i = 0; i < k; ++i)
+        {
+            /* af_xdp.c:217-223: the slot's UMEM address and the frame length */
+            struct xdp_desc *d = pb_ring_tx_desc(&x->tx, idx + i);
+            const uint32_t slot = (x->next_slot + i) & (x->n_frames - 1);
+            d->addr = (uint64_t)(x->slot_base + slot) * x->frame_size;
+            d->len = lens[sent + i];
+            d->options = 0;
+        }
+        pb_ring_prod_submit(&x->tx, k);
+        x->next_slot = (x->next_slot + k) & (x->n_frames - 1);
+        x->outstanding_tx += k;
+        (void)pb_xsk_complete(x, x->n_frames); /* af_xdp.c:233 */
+        sent += k;
     }
-    for (uint32_t i = 0; i < n; ++i)
-    {
-        /* af_xdp.c:217-223: the slot's UMEM address and the frame length */
-        struct xdp_desc *d = pb_ring_tx_desc(&x->tx, idx + i);
-        const uint32_t slot = (x->next_slot + i) & (x->n_frames - 1);
-        d->addr = (uint64_t)slot * x->frame_size;
-        d->len = lens[i];
-        d->options = 0;
-    }
-    pb_ring_prod_submit(&x->tx, n);
-    x->next_slot = (x->next_slot + n) & (x->n_frames - 1);
-    x->outstanding_tx += n;
-    (void)pb_xsk_complete(x, x->n_frames); /* af_xdp.c:233 */
     return 0;
 }

@@ -78,6 +78,10 @@ typedef struct pb_xsk
     int loop_auto;           /* loopback: pb_xsk_complete runs the kernel side inline (the wakeup) */
     void (*loop_sink)(void *ctx, const uint8_t *frame, uint32_t len, uint64_t addr);
     void *loop_ctx;
+    uint32_t batch;          /* TX descriptors per reserve / submit / complete (--batchsize); 0: all of a send */
+    uint32_t loop_hold;      /* loopback (tests): the kernel side leaves the newest loop_hold descriptors
+                                unconsumed, as a slow NIC would keep frames in flight */
+    uint32_t slot_base;      /* first UMEM slot of this queue's ring (--sharedumem: queues share one UMEM) */
 } pb_xsk_t;
 
 /* Loopback TX queue of n_frames (a power of two) slots of frame_size bytes over
@@ -94,10 +98,13 @@ uint32_t pb_xsk_loop_consume(pb_xsk_t *x, uint32_t max, pb_xsk_sink_fn sink, voi
 
 /* AF_XDP socket on (ifname, queue) over the UMEM, TX ring and completion ring
  * of n_frames entries.  bind_flags: XDP_COPY / XDP_ZEROCOPY / XDP_USE_NEED_WAKEUP
- * (af_xdp.c:289-330).  Returns 0, or -errno (EPERM without CAP_NET_RAW, EAFNOSUPPORT
- * without AF_XDP). */
+ * (af_xdp.c:289-330).  shared_fd >= 0: the UMEM is already registered on that
+ * socket (--sharedumem, af_xdp.c:412-428): this socket binds with
+ * XDP_SHARED_UMEM and its own fill / completion rings, and uses the n_frames
+ * slots from slot_base on.  Returns 0, or -errno (EPERM without CAP_NET_RAW,
+ * EAFNOSUPPORT without AF_XDP). */
 int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, uint32_t n_frames,
-                uint32_t frame_size, uint16_t bind_flags);
+                uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames);
 void pb_xsk_close(pb_xsk_t *x);
 
 /* complete_tx() (af_xdp.c:25-53): wake the kernel if it asks (or always without
@@ -108,9 +115,10 @@ uint32_t pb_xsk_complete(pb_xsk_t *x, uint32_t max);
 uint32_t pb_xsk_free_slots(const pb_xsk_t *x);
 
 /* send: `n` frames sit in UMEM slots next_slot, next_slot + 1, ... (mod n_frames)
- * with lengths lens[]; reserve n TX descriptors (reaping completions while the ring
- * is full, as send_packet does), fill {addr = slot * frame_size, len}, submit, and
- * complete once.  n <= pb_xsk_free_slots(); returns 0. */
+ * with lengths lens[]; in groups of `batch` descriptors (all n if 0): reserve them
+ * (reaping completions while the ring is full, as send_packet does), fill
+ * {addr = (slot_base + slot) * frame_size, len}, submit, complete once
+ * (af_xdp.c:184-233).  n <= pb_xsk_free_slots(); returns 0. */
 int pb_xsk_send(pb_xsk_t *x, const uint16_t *lens, uint32_t n);
 
 #ifdef __cplusplus

@@ -283,6 +283,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pbgpu_counters": (C.c_int, [P, U64P, U64P, C.c_int]),
         "pbgpu_kernel_time": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
         "pbgpu_set_timing": (C.c_int, [P, C.c_int]),
+        "pbgpu_kernel_times": (C.c_int, [P, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint32)]),
         "pbgpu_fill_probe": (C.c_int, [P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
         "pbgpu_fill_probe_ex": (C.c_int, [P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
         "pbgpu_fill_shape_name": (C.c_char_p, [C.c_int]),
@@ -419,6 +420,14 @@ class GpuContext:
         ms, n = C.c_double(), C.c_uint32()
         _check(self.lib.pbgpu_kernel_time(self.h, C.byref(ms), C.byref(n)), "kernel_time")
         return float(ms.value), int(n.value)
+
+    def kernel_times(self, cap: int = 4096) -> np.ndarray:
+        """TIMING_LAUNCH: each launch's device time (ms) since the last call."""
+        ms = np.zeros(cap, dtype=np.float64)
+        n = C.c_uint32()
+        _check(self.lib.pbgpu_kernel_times(self.h, ms.ctypes.data_as(C.POINTER(C.c_double)), cap, C.byref(n)),
+               "kernel_times")
+        return ms[:min(cap, int(n.value))]
 
     def fill_probe(self, nbytes: int, reps: int) -> float:
         ms = C.c_double()

@@ -47,7 +47,14 @@ def test_bench_json_line():
     assert d["config"]["workload"].startswith("c2_udp_64")
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
-    assert cb["cores"] == cb["host"]["affinity"] and cb["host"]["model"]
+    # the threads actually usable: the affinity mask capped by the cgroup CPU quota
+    q = cb["host"]["cgroup_cpu_quota"]
+    assert cb["cores"] == min(cb["host"]["affinity"], -(-q // 1) if q else cb["host"]["affinity"])
+    assert cb["host"]["model"] and d["cpu_baseline_variants"]["faithful_16_threads"]["cores"] == 16
+    # each launch timed on its own in a separate pass; the 1500-B leg >= 20 timed steps
+    for pl in (r["per_launch_ms"], d["udp_1500"]["per_launch_ms"]):
+        assert pl["n"] == 20 and 0 < pl["min"] <= pl["median"] <= pl["max"]
+    assert d["udp_1500"]["steps"] >= 20
     assert "not measured" in d["cpu_baseline_variants"]["configs0_c1_udp_static_64_1_thread"]["af_xdp_send"]
     assert d["udp_1500"]["kernel"].startswith("pb_fstage_kernel")
     # the write-roofline probe: every shape reported, the fastest named

@@ -1,0 +1,137 @@
+"""Round-3 GPU checks of behaviour around the kernels: counters that count work
+(sequence.c:633-653: every workgroup adds the frames it built and the bytes it
+stored), a rebuild of a buffer whose landing is still queued, and the drop-in
+binary's seeding (sequence.c:434-441)."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+import pb_configs as pc
+from pbgpu import GpuContext, Sequence
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "pb-af-xdp_amd", "bin", "pcktbatch-gpu")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = GpuContext(0)
+    yield c
+    c.close()
+
+
+def _count(ctx, name, n, first=0, idx=3):
+    seq = Sequence.from_config(pc.get(name))
+    ctx.load_sequence(idx, seq, pc.SEED_BASE)
+    fb = ctx.alloc_frames(*ctx.build_size(idx, n))
+    p0, b0 = ctx.counters(idx + 1)
+    ctx.build(idx, first, n, fb)
+    ctx.sync()
+    p1, b1 = ctx.counters(idx + 1)
+    total = fb.total_bytes()
+    kern = ctx.kernel_name(idx)
+    fb.free()
+    return int(p1[idx] - p0[idx]), int(b1[idx] - b0[idx]), total, kern
+
+
+# every kernel shape: the small / page / staged / variable / group-per-frame paths
+@pytest.mark.parametrize("name", ["c2_udp_64", "c4_tcp_syn", "c5_icmp_echo", "c1_udp_static_106", "c2_udp_1500",
+                                  "c3_udp_var", "udp_multi_payload", "udp_jumbo_var", "udp_fixed_odd_65",
+                                  "tcp_all_flags_var", "udp_tiny_var"])
+@pytest.mark.parametrize("n", [1, 777, 40000])
+def test_counters_count_built_frames_and_stored_bytes(ctx, name, n):
+    frames, stored, total, kern = _count(ctx, name, n, first=12345)
+    fpi = max(1, len(pc.get(name).get("payloads", [])))
+    assert frames == n * fpi, kern
+    assert stored == total, kern
+
+
+@pytest.mark.parametrize("name", ["c2_udp_1500", "c3_udp_var"])
+def test_skipped_stores_show_in_the_counters(ctx, name, monkeypatch):
+    """PBGPU_FST_DBG bit 1 builds without storing (a diagnostic): the frames are
+    counted, the bytes are not — the bench's counter check then fails."""
+    n = 50000
+    _, stored_ok, total, _ = _count(ctx, name, n)
+    assert stored_ok == total
+    monkeypatch.setenv("PBGPU_FST_DBG", "2")
+    frames, stored, _, kern = _count(ctx, name, n)
+    assert frames == n and stored == 0, kern
+    monkeypatch.delenv("PBGPU_FST_DBG")
+    assert _count(ctx, name, n)[1] == total
+
+
+def test_rebuild_waits_for_the_queued_landing(ctx):
+    """copy_to_umem_async from a buffer, then pbgpu_build into the same buffer at
+    once: the landed slots hold the first build's frames (the build stream waits
+    for the landing, pbgpu.h)."""
+    lib = ctx.lib
+    lib.pbgpu_copy_to_umem_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64,
+                                             C.c_uint32, C.POINTER(C.c_uint16)]
+    lib.pbgpu_land_wait.argtypes = [C.c_void_p, C.c_uint32]
+    seq = Sequence.from_config(pc.get("c2_udp_1500"))
+    ctx.load_sequence(5, seq, pc.SEED_BASE)
+    n = 4096
+    fb = ctx.alloc_frames(*ctx.build_size(5, n))
+    umem = np.zeros(4096 * n, dtype=np.uint8)
+    assert lib.pbgpu_host_register(ctx.h, umem.ctypes.data, umem.nbytes) == 0
+    lens = np.zeros(n, dtype=np.uint16)
+    try:
+        for rep in range(3):
+            ctx.build(5, rep * 10 * n, n, fb)
+            assert lib.pbgpu_copy_to_umem_async(ctx.h, fb.ptr, umem.ctypes.data, 4096, 0, 0, n,
+                                                lens.ctypes.data_as(C.POINTER(C.c_uint16))) == 0
+            for r2 in range(3):  # rebuild the same buffer while the landing is queued
+                ctx.build(5, rep * 10 * n + (r2 + 1) * n, n, fb)
+            assert lib.pbgpu_land_wait(ctx.h, 0) == 0
+            ctx.sync()
+            want = ob.frames(seq, 5, rep * 10 * n, 64, pc.SEED_BASE)
+            slots = umem.reshape(n, 4096)
+            for j in range(64):
+                assert slots[j, :1500].tobytes() == want[j]
+            assert (lens == 1500).all()
+    finally:
+        lib.pbgpu_host_unregister(ctx.h, umem.ctypes.data)
+        fb.free()
+
+
+def _pcap_frames(path):
+    raw = open(path, "rb").read()
+    out, p = [], 24
+    while p + 16 <= len(raw):
+        n = int.from_bytes(raw[p + 8:p + 12], "little")
+        out.append(raw[p + 16:p + 16 + n])
+        p += 16 + n
+    return out
+
+
+def test_binary_draws_a_seed_per_run_unless_given(tmp_path):
+    """pcktbatch-gpu without --seed: a fresh seed base per run (printed, replayable);
+    with --seed S: the same frames every run."""
+    def run(tag, *extra):
+        pcap = tmp_path / f"{tag}.pcap"
+        cmd = [BIN, "-z", "--interface", "pbnodev0", "--smac", pc.SMAC, "--dmac", pc.DMAC, "--dip", pc.DIP,
+               "--sip", "10.20.0.0/16", "--protocol", "udp", "--udport", "27015", "--pmin", "22", "--pmax", "22",
+               "--maxpckts", "200", "--delay", "0", "--gpubatch", "200", "--pcap", str(pcap), *extra]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, PB_SEQ_GAP_MS="0"))
+        assert r.returncode == 0, r.stderr
+        seed = [l for l in r.stdout.splitlines() if l.startswith("Seed base =>")]
+        assert len(seed) == 1
+        return _pcap_frames(pcap), seed[0]
+
+    a, sa = run("a")
+    b, sb = run("b")
+    assert len(a) == len(b) == 200 and sa != sb and a != b
+    c, _ = run("c", "--seed", "0x1234")
+    d, _ = run("d", "--seed", "0x1234")
+    assert c == d
+    # the printed seed replays the drawn run exactly
+    replay = sa.split("--seed ")[1].rstrip(").")
+    e, _ = run("e", "--seed", replay)
+    assert e == a

@@ -102,3 +102,23 @@ def test_two_pass_command_line():
     assert "queue_set=1 queue=3" in r.stdout and "batchsize=16 skb=1" in r.stdout
     assert "gpus=2 gpu=0 gpubatch=99 seed=77" in r.stdout and "pcap=/tmp/x.pcap" in r.stdout
     assert "10.20.0.0/16 -> 10.0.0.2 proto tcp" in r.stdout
+
+
+def test_seed_and_batch_flags_record_that_they_were_given():
+    lib = ours()
+    got = cb.parse(lib, cb.OurCmd, ["--seed", "0x10", "--veryrandom", "--batchsize", "32"],
+                   defaults=lib.cmd_line_af_xdp_defaults)
+    assert (got.seed_base, got.seed_set, got.very_random, got.batch_size, got.batch_set) == (16, 1, 1, 32, 1)
+    got = cb.parse(lib, cb.OurCmd, [], defaults=lib.cmd_line_af_xdp_defaults)
+    assert (got.seed_set, got.very_random, got.batch_size, got.batch_set) == (0, 0, 1, 0)
+
+
+def test_list_prints_a_drawn_seed_without_seed_flag():
+    """-l shows the seed base the run would use: drawn per run unless --seed is given."""
+    outs = [subprocess.run([BIN, "-z", "--dip", "10.0.0.2", "-l"], capture_output=True, text=True, timeout=60).stdout
+            for _ in range(2)]
+    seeds = [o.split("seed=")[1].split()[0] for o in outs]
+    assert seeds[0] != seeds[1]
+    o = subprocess.run([BIN, "-z", "--dip", "10.0.0.2", "--seed", "5", "-l"], capture_output=True, text=True,
+                       timeout=60).stdout
+    assert "seed=5 " in o

@@ -69,7 +69,8 @@ class Xsk(C.Structure):
                 ("tx", Ring), ("cq", Ring), ("fq", Ring), ("next_slot", C.c_uint32), ("outstanding_tx", C.c_uint32),
                 ("need_wakeup", C.c_uint32), ("wakeups", C.c_uint64), ("completed", C.c_uint64),
                 ("maps", C.c_void_p * 3), ("map_len", C.c_size_t * 3), ("loop_mem", C.c_void_p),
-                ("loop_auto", C.c_int), ("loop_sink", C.c_void_p), ("loop_ctx", C.c_void_p)]
+                ("loop_auto", C.c_int), ("loop_sink", C.c_void_p), ("loop_ctx", C.c_void_p), ("batch", C.c_uint32),
+                ("loop_hold", C.c_uint32), ("slot_base", C.c_uint32)]
 
 
 def _loopback(host, n, fs=4096):
@@ -143,12 +144,14 @@ def test_af_xdp_socket_setup_fails_cleanly_without_privilege(libs):
     x = Xsk()
     umem = np.zeros(4096 * 4096 + 4096, dtype=np.uint8)
     base = (umem.ctypes.data + 4095) & ~4095
-    rc = host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 4096, 8)
+    rc = host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096)
     # a negative errno (no AF_XDP / CAP_NET_RAW in this container), or a bound socket
     assert rc <= 0
     if rc == 0:
         host.pb_xsk_close(C.byref(x))
-    assert host.pb_xsk_open(C.byref(x), b"pbnodev0", 0, C.c_void_p(base), 4096, 4096, 8) == -19  # -ENODEV
+    assert host.pb_xsk_open(C.byref(x), b"pbnodev0", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096) == -19  # -ENODEV
+    # a shared-UMEM socket's slot range must lie inside the UMEM
+    assert host.pb_xsk_open(C.byref(x), b"lo", 1, C.c_void_p(base), 2048, 4096, 0, 3, 4096, 4096) == -22
 
 
 # ---------------------------------------------------------------- worker loop
@@ -346,3 +349,98 @@ def test_non_blocking_sequences_run_concurrently(libs):
     host.pb_sequence_totals(1, C.byref(p1), None)
     assert t_first < 0.5
     assert p1.value == 5000 and 0 < p0.value <= 5000
+
+
+# ---------------------------------------------------------------- AF_XDP flags (round 3)
+
+
+def test_send_submits_in_batches_of_batchsize(libs):
+    """--batchsize: descriptors per reserve / submit / complete (send_packet,
+    af_xdp.c:184-233); 0 (no --batchsize) submits a whole send at once."""
+    host, _ = libs
+    lens = (C.c_uint16 * 16)(*range(100, 116))
+    for batch, want_wakeups in ((0, 1), (4, 3), (1, 11)):
+        x, _keep = _loopback(host, 16)
+        x.batch = batch
+        assert host.pb_xsk_send(C.byref(x), lens, 11) == 0
+        assert x.completed == 11 and x.next_slot == 11 and x.wakeups == want_wakeups
+        host.pb_xsk_close(C.byref(x))
+
+
+def test_batchsize_flag_changes_the_worker_submits(libs):
+    host = libs[0]
+    w = {}
+    for kw in ({}, {"batch_size": 1, "batch_set": 1}, {"batch_size": 64, "batch_set": 1}):
+        r = _run(libs, _cfg(maxpckts=6000, delay=0), gpu_batch=3000, **kw)
+        assert r["pckts"] == 6000 and np.array_equal(r["k"], np.arange(6000, dtype=np.uint64))
+        d, c, wk = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        host.pb_sequence_tx_stats(0, C.byref(d), C.byref(c), C.byref(wk))
+        w[kw.get("batch_size", 0)] = wk.value
+    # one wakeup per submit: per landed chunk (<= 1024 frames), per frame, per 64 frames
+    # (landed chunks: 1024, 1024, 952 in the first batch; the second also splits at the ring's wrap)
+    assert w[1] == 6000 and 94 <= w[64] <= 100 and w[0] <= 12
+
+
+def test_sharedumem_gives_the_sequence_one_umem(libs):
+    """--sharedumem (af_xdp.c:412-428): the sequence's threads share one UMEM, each
+    in its own slot range; without it every thread allocates its own."""
+    host = libs[0]
+    for shared, want in ((0, 4), (1, 1)):
+        r = _run(libs, _cfg(maxpckts=20000, delay=0, threads=4), gpu_batch=1000, shared_umem=shared)
+        assert r["err"] == 0 and r["pckts"] == 20000 and len(np.unique(r["k"])) == 20000
+        assert (r["len"] != 0xFFFF).all()  # every descriptor's frame intact in its slot
+        u = C.c_uint64()
+        host.pb_sequence_umems(0, C.byref(u))
+        assert u.value == want
+
+
+def test_maxbytes_cut_never_rewrites_frames_in_flight(libs, monkeypatch):
+    """A max_bytes budget that ends inside a landed chunk stops the thread there:
+    no further landing may reuse the slots of frames still owned by the NIC (the
+    loopback holds PB_LOOP_HOLD descriptors unconsumed, as a slow NIC would)."""
+    monkeypatch.setenv("PB_LOOP_HOLD", "3000")
+    for maxb in (1_234_567, 3_000_001, 5_432_109):
+        r = _run(libs, _cfg(0, 1400, maxbytes=maxb, delay=0), gpu_batch=2000)
+        assert r["err"] == 0
+        n = r["seen"]
+        # every frame the NIC side consumed is the one its descriptor named, in order
+        assert np.array_equal(r["k"], np.arange(n, dtype=np.uint64))
+        assert (r["len"] != 0xFFFF).all()
+        assert maxb <= r["bytes"] < maxb + 1500 and r["pckts"] == n
+
+
+def test_skb_mode_is_copy_mode_and_refuses_zerocopy(libs):
+    host = libs[0]
+    host.pb_bind_flags.restype = C.c_uint16
+    host.pb_bind_flags.argtypes = [C.POINTER(OurCmd)]
+    host.pb_af_xdp_setup.argtypes = [C.POINTER(OurCmd), C.c_int]
+    XDP_COPY, XDP_ZEROCOPY, XDP_USE_NEED_WAKEUP = 2, 4, 8
+    assert host.pb_bind_flags(C.byref(_cmd(host))) == XDP_USE_NEED_WAKEUP
+    assert host.pb_bind_flags(C.byref(_cmd(host, skb_mode=1))) == XDP_COPY | XDP_USE_NEED_WAKEUP
+    assert host.pb_bind_flags(C.byref(_cmd(host, skb_mode=1, no_wake_up=1))) == XDP_COPY
+    assert host.pb_bind_flags(C.byref(_cmd(host, zero_copy=1))) == XDP_ZEROCOPY | XDP_USE_NEED_WAKEUP
+    assert host.pb_af_xdp_setup(C.byref(_cmd(host, skb_mode=1)), 0) == 0
+    assert host.pb_af_xdp_setup(C.byref(_cmd(host, skb_mode=1, zero_copy=1)), 0) == -22
+    assert host.pb_af_xdp_setup(C.byref(_cmd(host, batch_size=0, batch_set=1)), 0) == -22
+    binp = os.path.join(ROOT, "pb-af-xdp_amd", "bin", "pcktbatch-gpu")
+    r = subprocess.run([binp, "-z", "--dip", "10.0.0.2", "--skb", "--zerocopy"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode != 0 and "--skb and --zerocopy" in r.stderr
+
+
+def test_seed_is_drawn_per_run_unless_given(libs):
+    """Without --seed every run draws its seed base (CLOCK_BOOTTIME ns, or getrandom
+    with --veryrandom), as the reference seeds every iteration from the clock
+    (sequence.c:434-441); --seed S replays the same stream."""
+    host = libs[0]
+    host.pb_resolve_seed.restype = C.c_uint64
+    host.pb_resolve_seed.argtypes = [C.POINTER(OurCmd)]
+    a, b = _cmd(host), _cmd(host)
+    sa = host.pb_resolve_seed(C.byref(a))
+    time.sleep(0.001)
+    sb = host.pb_resolve_seed(C.byref(b))
+    assert sa != sb and a.seed_base == sa and b.seed_base == sb
+    r1, r2 = _cmd(host, very_random=1), _cmd(host, very_random=1)
+    assert host.pb_resolve_seed(C.byref(r1)) != host.pb_resolve_seed(C.byref(r2))
+    s1, s2 = _cmd(host, seed_base=1234, seed_set=1), _cmd(host, seed_base=1234, seed_set=1)
+    assert host.pb_resolve_seed(C.byref(s1)) == host.pb_resolve_seed(C.byref(s2)) == 1234
