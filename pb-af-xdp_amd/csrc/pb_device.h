@@ -141,6 +141,14 @@ struct pb_kargs
     // literal rule, several payloads: lit_stop[i] = min { j > i : setup data_len[j] <= j } (<= 64)
     const uint32_t *lit_stop;
     uint32_t small_wgt;     // pb_small_kernel's threads (= frames) per workgroup: 256 (0), 128 or 64
+    // pb_vline_kernel (packed variable lengths, every payload random, stream rule)
+    const uint32_t *orbit;  // LCG-orbit prefix sums: orbit[t] = {PE(8t), PO(8t)} mod 0xFFFF (u16 pair), t <= 2^21
+    uint32_t orbit_tot;     // PE(2^24) mod 0xFFFF (= PO(2^24)): runs that wrap the orbit
+    uint32_t vl;            // 1: launch pb_vline_kernel
+    uint32_t vl_wgf;        // its own frames per workgroup (<= 256 - PB_VST_GHOSTS)
+    uint32_t vl_nl48;       // lcg48 entries it keeps in LDS (chunks of the longest frame + 2)
+    uint32_t vl_nlines;     // its line-map entries (128-B lines of the longest workgroup region)
+    uint32_t sw_nw;         // >0: small fixed frames through pb_swin_kernel, sw_nw windows of 256 frames per workgroup
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)
@@ -165,6 +173,13 @@ struct pb_kargs
 #define PB_XS_XREMAP 0
 #endif
 #define PB_VST_CAP(wgf) (((size_t)(wgf) + PB_VST_GHOSTS + 1) & ~(size_t)1)
+// pb_vline_kernel's LDS: 256 B of prologue records, then per frame slot (own + ghosts) a 16-B
+// record and nsp 16-B header chunks, a zero chunk and 17 chunk masks, the lcg48 entries, the
+// line map (u16)
+#define PB_VL_STEP 16384u // bytes of a workgroup's region per step (4 waves x 4 KiB)
+#define PB_VL_LDS(wgf, nsp, nl48, nlines)                                                                     \
+    ((size_t)256 + ((size_t)(wgf) + PB_VST_GHOSTS) * 16 * (1 + (size_t)(nsp)) + 18 * 16 + (size_t)(nl48) * 8 + \
+     (((size_t)(nlines) + 7) & ~(size_t)7) * 2)
 #define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + PB_VST_PRO + PB_VST_CAP(wgf) * (PB_VST_HVN + 5) * 4 + (PB_VST_CAP(wgf) + 2) * 4)
 
 __device__ __forceinline__ uint32_t pb_mod(uint32_t n, const pb_div &v)

@@ -26,8 +26,8 @@
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st);
 extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
                                          uint64_t *offsets, hipStream_t st);
-extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t *bsum, uint32_t nblk, unsigned long long *l2,
-                                             uint32_t n_l2, uint64_t *offsets, hipStream_t st);
+extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t wgf, uint32_t *bsum, uint32_t nblk,
+                                             unsigned long long *l2, uint32_t n_l2, uint64_t *offsets, hipStream_t st);
 extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *offsets, uint64_t first, uint32_t n,
                                          uint8_t *dst, uint32_t stride, uint16_t *lens, hipStream_t st);
 extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipStream_t st);
@@ -133,8 +133,11 @@ struct pbgpu_ctx
     hipStream_t stream = nullptr;      // frame builds
     hipStream_t land_stream = nullptr; // UMEM landing: overlaps the next build (pbgpu_copy_to_umem)
     bool land_events = false;          // set by the first landing: builds then record a completion event
+    bool land_spin = true;             // pbgpu_land_wait polls (PBGPU_LAND_SPIN=0: blocking waits)
     uint2 *d_jump = nullptr;
     uint2 *d_lcg48 = nullptr;
+    uint32_t *d_orbit = nullptr; // pb_vline_kernel: LCG-orbit prefix sums (built on first use, 8 MiB)
+    uint32_t orbit_tot = 0;
     unsigned long long *d_dbg = nullptr; // PBGPU_TIMING: per-workgroup phase stamps
     uint64_t dbg_cap = 0;
     unsigned long long *d_counters = nullptr; // [PB_MAX_SEQUENCES][PB_CTR_SHARDS][PB_CTR_STRIDE]
@@ -229,6 +232,31 @@ std::vector<uint2> make_jump_table()
         A = a3 * A;
         C = a3 * C + c3;
     }
+    return t;
+}
+
+// pb_vline_kernel's payload sums (pbgpu_kernels.hip, pb_orbit_sum): M = L^3 mod 2^24 walks one
+// orbit of all 2^24 states from 0 (full period: c odd, a = 1 mod 4); entry t holds the sums of
+// the bytes (bits 16-23) at the even and the odd positions before 8t, mod 0xFFFF, as two u16.
+std::vector<uint32_t> make_orbit_table(uint32_t *total)
+{
+    const uint32_t m = 0xFFFFFFu;
+    const uint32_t a3 = (PB_LCG_A * PB_LCG_A * PB_LCG_A) & m, c3 = (PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u)) & m;
+    std::vector<uint32_t> t((1u << 21) + 1);
+    uint32_t y = 0, pe = 0, po = 0;
+    for (uint32_t k = 0; k < (1u << 24); ++k)
+    {
+        if ((k & 7u) == 0)
+            t[k >> 3] = pe | (po << 16);
+        const uint32_t b = (y >> 16) & 0xFFu;
+        if (k & 1u)
+            po = (po + b) % 0xFFFFu;
+        else
+            pe = (pe + b) % 0xFFFFu;
+        y = (a3 * y + c3) & m;
+    }
+    t[1u << 21] = pe | (po << 16);
+    *total = pe; // the even and odd totals are equal (each byte value 2^15 times per parity)
     return t;
 }
 
@@ -401,6 +429,7 @@ int pbgpu_open(int device, pbgpu_ctx **out)
     HIPCHK(hipSetDevice(device));
     pbgpu_ctx *ctx = new pbgpu_ctx();
     ctx->device = device;
+    ctx->land_spin = !env_is("PBGPU_LAND_SPIN", "0");
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->land_stream, hipStreamNonBlocking) != hipSuccess)
     {
@@ -465,6 +494,8 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipFree(ctx->d_jump);
     if (ctx->d_lcg48)
         (void)hipFree(ctx->d_lcg48);
+    if (ctx->d_orbit)
+        (void)hipFree(ctx->d_orbit);
     if (ctx->d_dbg)
         (void)hipFree(ctx->d_dbg);
     if (ctx->d_counters)
@@ -789,6 +820,10 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             if (enp > 0 && (uint32_t)enp * K.xp_fpp <= 2 * PB_WG)
                 K.xs_np = (uint32_t)enp;
         }
+        // windowed form (pb_swin_kernel) for the lengths the page kernels do not take: PBGPU_SMALL_WIN
+        // = windows of 256 frames per workgroup (0: the linear pb_small_kernel)
+        if (!K.xs_np || env_is("PBGPU_KERNEL", "linear"))
+            K.sw_nw = (uint32_t)std::min(64, std::max(0, env_int("PBGPU_SMALL_WIN", 0)));
         if (!pls[0].random)
         {
             const uint32_t p0 = (K.hl - 2) / 4;
@@ -945,6 +980,43 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             // PBGPU_FST_G, PBGPU_FST_WGF, PBGPU_FST_NBUF override the shape.
             const bool fst_ok = K.fixed_len && minf > 128 && minf % 4 == 0 && K.gpf_rmode == 1 &&
                                 !(flags & PBK_LITERAL) && !gpf_only && !env_is("PBGPU_KERNEL", "stage");
+            // packed variable lengths, every payload random, stream rule, payloads of >= 32 B:
+            // pb_vline_kernel (no LDS stage).  ICMP type 0 / code 0 is left to
+            // pb_vstage_kernel: its header word sum can be 0, where the orbit sums cannot tell a
+            // zero payload sum from 0xFFFF.  PBGPU_KERNEL=vstage keeps pb_vstage_kernel.
+            const bool icmp00 = proto == 1 && t[34] == 0 && t[35] == 0;
+            if (!K.fixed_len && K.gpf_rmode == 1 && !(flags & PBK_LITERAL) && !gpf_only && minf >= K.hl + 32 &&
+                maxf <= 4096 && !icmp00 && !env_is("PBGPU_KERNEL", "vstage") && !env_is("PBGPU_KERNEL", "stage"))
+            {
+                const uint32_t nsp = K.hl == 54 ? 5u : 4u;
+                uint32_t wf = (uint32_t)env_int("PBGPU_VL_WGF", PB_WG - PB_VST_GHOSTS);
+                wf = std::max(32u, std::min<uint32_t>(wf, PB_WG - PB_VST_GHOSTS));
+                uint32_t nl48 = 0, nlines = 0;
+                for (;; wf -= 4)
+                {
+                    const uint64_t rmax = (uint64_t)wf * maxf + 256; // own frames + the line before the first
+                    nl48 = (maxf + 31) / 16 + 1;
+                    nlines = (uint32_t)(rmax / 128 + 2);
+                    if (PB_VL_LDS(wf, nsp, nl48, nlines) <= 40 * 1024 || wf <= 32) // >= 4 workgroups per CU
+                        break;
+                }
+                if (ctx->d_orbit == nullptr)
+                {
+                    uint32_t tot = 0;
+                    std::vector<uint32_t> orb = make_orbit_table(&tot);
+                    int rc2 = upload(&ctx->d_orbit, orb.data(), orb.size());
+                    if (rc2 != PBGPU_OK)
+                        return rc2;
+                    ctx->orbit_tot = tot;
+                }
+                K.vl = 1;
+                K.vl_wgf = wf;
+                K.vl_nl48 = nl48;
+                K.vl_nlines = nlines;
+                K.orbit = ctx->d_orbit;
+                K.orbit_tot = ctx->orbit_tot;
+                K.fst_dbg = (uint32_t)env_int("PBGPU_FST_DBG", 0);
+            }
             if (fst_ok)
             {
                 const uint32_t eg = (uint32_t)env_int("PBGPU_FST_G", 0);
@@ -1181,15 +1253,18 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         K.vblk_sum = nullptr;
         K.vblk_l2 = nullptr;
         K.offsets_w = nullptr;
-        if (K.vst && K.stage_wgf >= PB_VST_SCAN_MIN_WGF && !env_is("PBGPU_VST_SCAN", "3pass"))
+        const uint32_t wgf = K.vl ? K.vl_wgf : K.stage_wgf;
+        if (K.vl || (K.vst && K.stage_wgf >= PB_VST_SCAN_MIN_WGF && !env_is("PBGPU_VST_SCAN", "3pass")))
         {
-            // pb_vstage_kernel: per-workgroup length sums, their scan, offsets written by the build
-            const uint64_t nblk = (nf + K.stage_wgf - 1) / K.stage_wgf;
+            // pb_vline_kernel / pb_vstage_kernel: per-workgroup length sums, their scan, offsets
+            // written by the build
+            const uint64_t nblk = (nf + wgf - 1) / wgf;
             const uint64_t n_l2 = (nblk + 255) / 256;
             uint32_t *bsum = reinterpret_cast<uint32_t *>(out->scan_tmp);
             unsigned long long *l2 =
                 reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(out->scan_tmp) + vst_bsum_bytes(nblk));
-            HIPCHK(pbk_launch_vst_lengths(&K, bsum, (uint32_t)nblk, l2, (uint32_t)n_l2, out->offsets, ctx->stream));
+            HIPCHK(pbk_launch_vst_lengths(&K, wgf, bsum, (uint32_t)nblk, l2, (uint32_t)n_l2, out->offsets,
+                                          ctx->stream));
             K.vblk_sum = bsum;
             K.vblk_l2 = l2;
             K.offsets_w = out->offsets;
@@ -1378,7 +1453,14 @@ int pbgpu_land_wait(pbgpu_ctx *ctx, uint32_t keep)
     while (ctx->landings.size() > keep)
     {
         pbgpu_ctx::land_op op = ctx->landings.front();
-        const hipError_t e = hipEventSynchronize(op.ev);
+        // a sender waits on every landing: poll the event rather than block in the runtime
+        // (a blocking wait adds its wake-up latency to each landing; PBGPU_LAND_SPIN=0 blocks)
+        hipError_t e = hipSuccess;
+        if (ctx->land_spin)
+            while ((e = hipEventQuery(op.ev)) == hipErrorNotReady)
+                ;
+        else
+            e = hipEventSynchronize(op.ev);
         ctx->landings.pop_front();
         ctx->land_pool.push_back(op.ev);
         if (e != hipSuccess)
@@ -1708,7 +1790,9 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
     if (!S.loaded)
         return PBGPU_ENOENT;
     const pb_kargs &K = S.K;
-    if (K.fst_g)
+    if (K.vl)
+        snprintf(buf, n, "pb_vline_kernel<%u, %u>", K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
+    else if (K.fst_g)
         snprintf(buf, n, "pb_fstage_kernel<%u, %u>", K.fst_g, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
     else if (K.stage_win && K.vst)
         snprintf(buf, n, "pb_vstage_kernel<%u, %u>", K.gpf_g, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
@@ -1716,6 +1800,8 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
+    else if (K.sw_nw)
+        snprintf(buf, n, "pb_swin_kernel<%u, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
     else if (K.xs_np && !env_is("PBGPU_KERNEL", "linear"))
         snprintf(buf, n, "%s<%u, %u, %s>", K.xp ? "pb_xpage_kernel" : "pb_xsmall_kernel", K.small_ndw, K.proto,
                  K.pl0.random ? "true" : "false");

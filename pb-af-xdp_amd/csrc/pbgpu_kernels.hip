@@ -516,6 +516,62 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
         pb_count(K, blockIdx.x, nfr, tile_bytes);
 }
 
+// Windowed form (the 98-B ICMP and 106-B UDP frames of configs[4] / configs[0], every other fixed
+// length <= 128 B that pb_xsmall_kernel / pb_xpage_kernel do not take): a workgroup owns a
+// region of NW windows of 256 frames (XCD-contiguous regions, pb_xcd_region) and builds them one
+// window at a time — one lane per frame into the LDS tile, a barrier, the window's bytes out as
+// 16-B stores whose absolute chunk index is the lane (each wave store one 1-KiB-aligned block),
+// a barrier.  The linear form's 64-frame (6 KiB) workgroups write the 64-thread-workgroup store
+// shape (<= 6.4 TB/s in profiles/r02/wbench), where a long region walked in order by each XCD
+// reaches the staged 1500-B kernel's 6.6-7.0 TB/s.  256 frames of even length end on a 128-B
+// line, so no line has two writers.
+template <int NDW, int PROTO, bool RANDOM>
+__global__ __launch_bounds__(PB_WG) void pb_swin_kernel(pb_kargs K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[PB_WG * NDW + 8];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nw = K.sw_nw;
+    const uint32_t bxr = pb_xcd_region(blockIdx.x, gridDim.x);
+    const uint32_t flen = K.fixed_len;
+    const uint64_t fr0 = (uint64_t)bxr * nw * PB_WG;
+    const bool swz = (flen & 7u) == 0;
+    uint32_t built = 0;
+    for (uint32_t w = 0; w < nw; ++w)
+    {
+        const uint64_t f0 = fr0 + (uint64_t)w * PB_WG;
+        if (f0 >= K.n_frames)
+            break;
+        const uint64_t left = K.n_frames - f0;
+        const uint32_t nfr = left < PB_WG ? (uint32_t)left : PB_WG;
+        if (tid < nfr)
+        {
+            uint32_t d[NDW];
+            pb_small_frame<NDW, PROTO, RANDOM>(K, f0 + tid, d);
+            pb_small_put<NDW>(s_tile, d, tid * flen, flen);
+        }
+        __syncthreads();
+        const uint32_t tile_bytes = nfr * flen;
+        const uint32_t nchunks = (tile_bytes + 15) >> 4;
+        const uint64_t ob = f0 * flen; // 16-B aligned (256 frames of any length are)
+        uint8_t *const out = K.out + ob;
+        for (uint32_t c = (tid - (uint32_t)(ob >> 4)) & (PB_WG - 1u); c < nchunks; c += PB_WG)
+        {
+            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[swz ? pb_swz(c) : c];
+            if (16 * c + 16 > tile_bytes) // last chunk of the stream: zero the tail
+            {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    v[t] &= pb_range_mask(0, (int)tile_bytes - (int)(16 * c + 4 * t));
+            }
+            pb_st16(out + 16 * c, v);
+        }
+        built += nfr;
+        __syncthreads(); // the next window reuses the tile
+    }
+    if (tid == 0)
+        pb_count(K, bxr, built, (uint64_t)built * flen);
+}
+
 // XCD-owned form, for frame lengths that divide 4096 (64-B configs[1] frames,
 // 128-B frames).  The output stream (4 KiB aligned) is cut into 4 KiB pages of
 // fp = 4096 / flen whole frames; workgroup b, which the dispatcher deals to XCD
@@ -1995,6 +2051,341 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         pb_count(K, bxr, nown, (K.fst_dbg & 2u) ? 0ull : hi_abs - lo_abs);
 }
 
+// ---------------- packed variable lengths, stores straight from registers: pb_vline_kernel ----------------
+//
+// configs[2].  pb_vstage_kernel assembles every window in an LDS stage between
+// three barriers and spends ~200 VALU per (lane, frame) on setting up a group of lanes for each
+// frame; here nothing is staged and the workgroup's waves never meet after the prologue:
+//  * prologue (one lane per frame slot: up to PB_VST_GHOSTS earlier frames, then the own frames):
+//    seed, fields, header image with both checksums — the L4 payload sum without the payload
+//    bytes, from prefix sums over the LCG's orbit (pb_orbit_sum) — the start from a workgroup
+//    scan, then per frame a 16-B record {start, end, LCG state at its first chunk} and its header
+//    bytes already shifted to the frame's position in its first NSP 16-B chunks; a u16 map of the
+//    region's 128-B lines to the frame holding each line's first byte;
+//  * stream: the workgroup's byte region [lo, hi) (128-B aligned: no line has two writers) in
+//    16-KiB steps, wave w writing bytes [4 KiB w, 4 KiB (w + 1)) of a step as four 1-KiB store
+//    instructions (lane l: chunk l of each KiB).  A chunk that lies inside one frame's payload
+//    ("pure") is generated from the frame's record (line map -> record -> L^(48 m) entry) and
+//    stored; the others — the few chunks that hold header bytes or a frame edge — are left out,
+//    and after each step's payload chunks a pair of waves writes the "special" chunks of the
+//    frames whose first chunk lies in the step: header chunk | the previous frame's payload tail
+//    | the frame's own first payload bytes, each from one generated chunk and a mask.
+// Every byte of [lo, hi) is stored exactly once, whole 16-B chunks only (the launch's last chunk
+// zero-padded past the last frame).  Requires payloads of >= 32 bytes (a chunk then holds bytes
+// of at most two frames, and never a payload end and the next header end).
+// The L4 payload sum: payload byte j is bits 16-23 of M^(j+1)(st0), M = L^3 mod 2^24 (full
+// period), so a payload is a run of consecutive orbit positions [p, p + n) of M, p = the discrete
+// log of M(st0) (24 fixed steps, the PCG "distance" construction), and its word sum is a
+// difference of prefix sums of the orbit's even- and odd-position bytes (K.orbit, every 8th
+// position, <= 7 LCG steps at each end).
+
+// discrete-log constants: M^(2^i) as (a_i, c_i) mod 2^24
+constexpr uint32_t PB_M24 = 0xFFFFFFu;
+constexpr uint32_t pb_orb_a(int i)
+{
+    uint32_t a = PB_A3 & PB_M24;
+    for (int k = 0; k < i; ++k)
+        a = (a * a) & PB_M24;
+    return a;
+}
+constexpr uint32_t pb_orb_c(int i)
+{
+    uint32_t a = PB_A3 & PB_M24, c = PB_C3 & PB_M24;
+    for (int k = 0; k < i; ++k)
+    {
+        c = ((a + 1u) * c) & PB_M24;
+        a = (a * a) & PB_M24;
+    }
+    return c;
+}
+
+// Little-endian 16-bit word sum (mod 0xFFFF, in [1, 0xFFFF]) of the n >= 3 payload bytes drawn
+// from the LCG state st0 entering the payload (sequence.c:552-555), payload at an even L4 offset:
+// the value fold(sum of the bytes' words) takes (the orbit has no run of 3 zero bytes, so the true
+// sum is never 0).
+__device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0, uint32_t n)
+{
+    const uint32_t yp = (PB_A3 * st0 + PB_C3) & PB_M24; // the state of payload byte 0
+    uint32_t cur = 0, p = 0;
+#pragma unroll
+    for (int i = 0; i < 24; ++i)
+    {
+        const uint32_t bit = 1u << i;
+        const uint32_t nx = __umul24(cur, pb_orb_a(i)) + pb_orb_c(i);
+        const bool take = ((cur ^ yp) & bit) != 0;
+        cur = take ? nx : cur;
+        p |= take ? bit : 0u;
+    }
+    const uint2 jq = K.jump[n - 1 + PB_JNEG]; // L^(3n): the state one past the payload
+    const uint32_t yq = jq.x * yp + jq.y;
+    uint32_t q = p + n, wrap = 0;
+    if (q >= (1u << 24)) // the run wraps the orbit (2^24 is even: parities keep)
+        q -= 1u << 24, wrap = K.orbit_tot;
+    const uint32_t tp = K.orbit[(p + 7) >> 3], tq = K.orbit[(q + 7) >> 3];
+    // prefix sums at p and q from the next sampled position, minus the bytes in between
+    uint32_t e_p = 0, o_p = 0, e_q = 0, o_q = 0;
+    uint32_t y = yp, z = yq;
+    const uint32_t cp = (8u - (p & 7u)) & 7u, cq = (8u - (q & 7u)) & 7u;
+#pragma unroll
+    for (uint32_t t = 0; t < 7; ++t)
+    {
+        const uint32_t bp = t < cp ? (y >> 16) & 0xFFu : 0u, bq = t < cq ? (z >> 16) & 0xFFu : 0u;
+        if ((p + t) & 1u)
+            o_p += bp;
+        else
+            e_p += bp;
+        if ((q + t) & 1u)
+            o_q += bq;
+        else
+            e_q += bq;
+        y = __umul24(y, PB_A3) + PB_C3;
+        z = __umul24(z, PB_A3) + PB_C3;
+    }
+    // PE(q) - PE(p), PO(q) - PO(p), kept positive with multiples of 0xFFFF
+    const uint32_t de = (tq & 0xFFFFu) + wrap + e_p + 2u * 0xFFFFu - e_q - (tp & 0xFFFFu);
+    const uint32_t dO = (tq >> 16) + wrap + o_p + 2u * 0xFFFFu - o_q - (tp >> 16);
+    // payload byte j sits at orbit position p + j: even j is a word's low byte
+    const uint32_t s = (p & 1u) ? dO + (de << 8) : de + (dO << 8);
+    return pb_fold(s);
+}
+
+template <int HL, bool L4>
+__global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
+{
+    constexpr uint32_t GH = PB_VST_GHOSTS;
+    constexpr uint32_t NSP = (15 + HL + 15) / 16; // chunks a frame's header can touch
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    const uint32_t WF = K.vl_wgf;
+    const uint32_t CAP = WF + GH;
+    uint2 *const s_jt = reinterpret_cast<uint2 *>(s_dyn);             // jump[PB_JNEG - (i + HL)], i < 16
+    uint64_t *const s_st0 = reinterpret_cast<uint64_t *>(s_dyn + 32); // [0, GH]: slot starts - base0; [8, 12): S0 parts
+    uint32_t *const s_wsum = s_dyn + 56;                              // per-wave length sums
+    pb_u32x4 *const s_rec = reinterpret_cast<pb_u32x4 *>(s_dyn + 64); // {start, end, z, -} per frame slot
+    pb_u32x4 *const s_img = s_rec + CAP;                              // NSP header chunks per frame slot
+    pb_u32x4 *const s_m16 = s_img + CAP * NSP + 1;                    // after one zero chunk: byte masks
+    uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_m16 + 17);
+    uint16_t *const s_map = reinterpret_cast<uint16_t *>(s_l48 + K.vl_nl48);
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t bxr = pb_xcd_region(blockIdx.x, gridDim.x); // XCD x walks the x-th eighth of the regions
+    const uint32_t flags = K.flags;
+    const uint64_t f0 = (uint64_t)bxr * WF;
+    const uint64_t left = K.n_frames - f0;
+    const uint32_t nown = left < WF ? (uint32_t)left : WF;
+    const uint64_t fe = f0 + nown;
+
+    // ---------------- prologue: one lane per frame slot ----------------
+    const int64_t fb = (int64_t)f0 - (int64_t)GH;
+    uint64_t s0_part = 0;
+    if (tid < (bxr & 255u))
+        s0_part = K.vblk_sum[(bxr & ~255u) + tid];
+    const uint64_t s0_base = K.vblk_l2[bxr >> 8];
+    uint2 jtv = make_uint2(0u, 0u);
+    if (tid < 16u)
+        jtv = K.jump[PB_JNEG - (tid + HL)];
+    for (uint32_t i = tid; i < K.vl_nl48; i += PB_WG)
+        s_l48[i] = K.lcg48[i];
+    const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
+    const int64_t fj = fb + (int64_t)tid;
+    const bool valid = tid < CAP && fj >= 0 && (uint64_t)fj < fe;
+    uint32_t flen = 0, st0 = 0;
+    uint32_t d[16];
+#pragma unroll
+    for (int w = 0; w < 16; ++w)
+        d[w] = 0u;
+    if (valid)
+    {
+        uint64_t k;
+        uint32_t pi;
+        pb_frame_index(K, (uint64_t)fj, k, pi);
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+        const uint32_t r0 = pb_rand_r(s);
+        const pb_frame_pl P = pb_payload<false>(K, s, pi);
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
+        flen = HL + P.plen;
+        st0 = P.st0;
+        if (L4)
+        {
+            // csum_tcpudp_magic / icmp_csum (sequence.c:569-594): header (+ pseudo header) words
+            // plus the payload's, from the orbit prefix sums
+            uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) + pb_halves(d[12]) +
+                          pb_halves(d[13]);
+            if (flags & PBK_PSEUDO)
+                hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
+            const uint32_t c = (~pb_fold(pb_fold(hs) + pb_orbit_sum(K, P.st0, P.plen))) & 0xFFFFu;
+            const uint32_t cv = K.csum_hi ? (c << 16) : c;
+#pragma unroll
+            for (uint32_t w = 0; w < 16; ++w)
+                d[w] |= w == K.csum_dw ? cv : 0u;
+        }
+    }
+    // frame starts: exclusive scan of the slot lengths (in-wave shuffles, wave totals via LDS)
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    uint32_t inc = flen;
+#pragma unroll
+    for (uint32_t dd = 1; dd < 64; dd <<= 1)
+    {
+        const uint32_t y = __shfl_up(inc, dd, 64);
+        inc += lane >= dd ? y : 0u;
+    }
+#pragma unroll
+    for (uint32_t dd = 32; dd > 0; dd >>= 1)
+        s0_part += __shfl_xor(s0_part, dd, 64);
+    if (lane == 63u)
+        s_wsum[wv] = inc;
+    if (lane == 0u)
+        s_st0[8 + wv] = s0_part;
+    if (tid <= GH)
+        s_st0[tid] = inc - flen;
+    if (tid < 16u)
+        s_jt[tid] = jtv;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < PB_WG / 64; ++w)
+    {
+        const uint32_t t = s_wsum[w];
+        pre += w < wv ? t : 0u;
+        tot += t;
+    }
+    uint64_t S0 = s0_base;
+#pragma unroll
+    for (uint32_t w = 0; w < PB_WG / 64; ++w)
+        S0 += s_st0[8 + w];
+    const uint64_t base0 = S0 - s_st0[GH]; // start of slot 0
+    const uint64_t start = base0 + pre + (inc - flen);
+    if (valid && tid >= GH) // own frames: the offsets
+        K.offsets_w[(uint64_t)fj] = start;
+    // region [lo, hi): lo = the 128-B line of the first own frame's start (0 for the first region),
+    // hi = the next region's lo (the launch's end for the last)
+    const bool last = fe == K.n_frames;
+    const uint64_t lo_abs = bxr ? (S0 & ~127ull) : 0ull;
+    const uint64_t hi_abs = last ? base0 + tot : ((base0 + tot) & ~127ull);
+    // ghosts: the frames before f0 that end past lo (a prefix f0 - 1, f0 - 2, ...)
+    uint32_t ng = 0;
+    if (bxr)
+        while (ng < GH && f0 > ng && base0 + s_st0[GH - ng] > lo_abs)
+            ++ng;
+    const uint32_t nfr = ng + nown; // frames with records: slot index t = tid - (GH - ng)
+    const uint64_t wbase = (base0 + s_st0[GH - ng]) & ~15ull;
+    const uint32_t lo_rel = (uint32_t)(lo_abs - wbase), hi_rel = (uint32_t)(hi_abs - wbase);
+    const int32_t tix = (int32_t)tid - (int32_t)(GH - ng);
+    if (valid && tix >= 0)
+    {
+        const uint32_t r = (uint32_t)(start - wbase);
+        const uint32_t s0 = r & 15u;
+        const uint2 jt = s_jt[s0];
+        s_rec[tix] = pb_u32x4{r, r + flen, jt.x * st0 + jt.y, 0u};
+        // the header image shifted to byte s0 of the frame's first chunk: out dword u holds image
+        // bytes [4u - s0, 4u - s0 + 4)
+        const uint32_t q = s0 >> 2, sh = s0 & 3u;
+        uint32_t v[17];
+#pragma unroll
+        for (int u = 0; u < 17; ++u)
+        {
+            const uint32_t lo = u > 0 ? d[u - 1] : 0u, hi = u < 16 ? d[u] : 0u;
+            v[u] = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
+        }
+        pb_u32x4 *const img = s_img + (uint32_t)tix * NSP;
+#pragma unroll
+        for (uint32_t j = 0; j < NSP; ++j)
+        {
+            uint32_t o[4];
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t)
+            {
+                const int u = (int)(4 * j + t);
+                const uint32_t a0 = u < 17 ? v[u] : 0u;
+                const uint32_t a1 = u >= 1 && u - 1 < 17 ? v[u - 1] : 0u;
+                const uint32_t a2 = u >= 2 && u - 2 < 17 ? v[u - 2] : 0u;
+                const uint32_t a3 = u >= 3 && u - 3 < 17 ? v[u - 3] : 0u;
+                o[t] = q == 0 ? a0 : (q == 1 ? a1 : (q == 2 ? a2 : a3));
+            }
+            img[j] = pb_u32x4{o[0], o[1], o[2], o[3]};
+        }
+    }
+    __syncthreads();
+
+    // line map
+    const uint32_t R = hi_rel - lo_rel;
+    const uint32_t nlines = (R + 127u) >> 7;
+    if ((uint32_t)tix < nfr && tix >= 0)
+    {
+        const pb_u32x4 rc = s_rec[tix];
+        // lines whose first byte lies in this frame: the frame holding it, and where (if at all)
+        // the next frame starts in the line
+        const uint32_t a = rc[0] > lo_rel ? rc[0] - lo_rel : 0u, b = rc[1] > lo_rel ? rc[1] - lo_rel : 0u;
+        const uint32_t la = (a + 127u) >> 7, lb = min((b + 127u) >> 7, nlines);
+        // the next two frames' starts in the line as 16-B chunk positions ceil(o / 16) (1..8; 15:
+        // none): a chunk k of the line lies in frame tix + (k >= c1) + (k >= c2)
+        const uint32_t b2 = (uint32_t)tix + 1u < nfr ? s_rec[tix + 1][1] - lo_rel : 0xFFFFFFFFu;
+        for (uint32_t L = la; L < lb; ++L)
+        {
+            const uint32_t o1 = b - (L << 7), o2 = b2 - (L << 7);
+            const uint32_t c1 = o1 < 128u ? (o1 + 15u) >> 4 : 15u, c2 = o2 < 128u ? (o2 + 15u) >> 4 : 15u;
+            s_map[L] = (uint16_t)((uint32_t)tix | (c1 << 8) | (c2 << 12));
+        }
+    }
+    if (tid <= 16u) // chunk byte masks: s_m16[k] keeps bytes >= k
+        s_m16[tid] = pb_u32x4{pb_range_mask((int)tid, 4), pb_range_mask((int)tid - 4, 4), pb_range_mask((int)tid - 8, 4),
+                              pb_range_mask((int)tid - 12, 4)};
+    if (tid == 32u)
+        s_img[CAP * NSP] = pb_u32x4{0u, 0u, 0u, 0u}; // the zero header chunk
+    __syncthreads();
+
+    // ---------------- stream: the region in 16-KiB steps, no barriers ----------------
+    // Chunk at region offset c (absolute pos = lo + c): frame f holds its first byte, g = f + 1
+    // may start inside it.  Its bytes = f's payload bytes in [max(S_f + HL, pos), min(E_f, pos + 16))
+    // (one generated chunk, masked) | f's header bytes if the chunk is one of f's first NSP (the
+    // shifted image) | g's header bytes if g starts inside the chunk (g's first image chunk):
+    // one straight-line path for every chunk, and every 128-B line leaves in one store instruction.
+    const uint32_t zero = CAP * NSP;
+    uint8_t *const gout = K.out + wbase;
+    const bool store = !(K.fst_dbg & 2u);
+    const uint32_t nsteps = (R + PB_VL_STEP - 1u) / PB_VL_STEP;
+    for (uint32_t s = 0; s < nsteps; ++s)
+    {
+        // four independent chunks per lane, computed before any is stored (straight-line: their
+        // LDS reads and LCG chains overlap); chunks past the region's end are computed on chunk 0
+        // and not stored
+        pb_u32x4 v[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+        {
+            const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
+            const uint32_t c = c0 < R ? c0 : 0u;
+            const uint32_t pos = lo_rel + c;
+            const uint32_t e = s_map[c >> 7], k = (c >> 4) & 7u;
+            const uint32_t f = (e & 0xFFu) + (k >= ((e >> 8) & 15u) ? 1u : 0u) + (k >= (e >> 12) ? 1u : 0u);
+            const pb_u32x4 rc = s_rec[f];
+            const uint32_t cb = rc[0] & ~15u;
+            const uint32_t m = (pos - cb) >> 4; // chunk index within frame f
+            const uint2 L = s_l48[m];
+            const uint32_t x = __umul24(rc[2], L.x) + L.y;
+            const uint32_t plo = rc[0] + HL > pos ? min(rc[0] + HL - pos, 16u) : 0u;
+            const uint32_t phi = min(rc[1] - pos, 16u);
+            const bool g_in = phi < 16u && f + 1u < nfr; // the next frame starts inside the chunk
+            const pb_u32x4 ha = s_img[m < NSP ? f * NSP + m : zero];
+            const pb_u32x4 hb = s_img[g_in ? (f + 1u) * NSP : zero];
+            const pb_u32x4 ml = s_m16[plo], mh = s_m16[phi];
+            uint32_t o0 = x, o1 = x, o2 = x, o3 = x;
+            if (!(K.fst_dbg & 1u)) // (PBGPU_FST_DBG bit 0, diagnostics only: no payload generation)
+                pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+            v[i] = pb_u32x4{(o0 & ml[0] & ~mh[0]) | ha[0] | hb[0], (o1 & ml[1] & ~mh[1]) | ha[1] | hb[1],
+                            (o2 & ml[2] & ~mh[2]) | ha[2] | hb[2], (o3 & ml[3] & ~mh[3]) | ha[3] | hb[3]};
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+        {
+            const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
+            if (store && c0 < R)
+                pb_st16(gout + lo_rel + c0, v[i]);
+        }
+    }
+    if (tid == 0) // the workgroup stores exactly [lo, hi) (the launch's last chunk zero-padded)
+        pb_count(K, bxr, nown, store ? hi_abs - lo_abs : 0ull);
+}
+
 // ---------------- variable length: lengths -> offsets -> tile map ----------------
 
 __global__ __launch_bounds__(256) void pb_len_reduce(pb_kargs K, unsigned long long *block_sums)
@@ -2158,7 +2549,15 @@ __global__ __launch_bounds__(256) void pb_fill_kernel(pb_u32x4 *dst, uint64_t n1
 template <int NDW, int PROTO>
 static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
 {
-    if (K->xs_grid && K->xp)
+    if (K->sw_nw && !K->xs_grid)
+    {
+        const uint32_t g = (uint32_t)((K->n_frames + (uint64_t)K->sw_nw * PB_WG - 1) / ((uint64_t)K->sw_nw * PB_WG));
+        if (K->pl0.random)
+            hipLaunchKernelGGL((pb_swin_kernel<NDW, PROTO, true>), dim3(g), dim3(PB_WG), K->lds_pad, st, *K);
+        else
+            hipLaunchKernelGGL((pb_swin_kernel<NDW, PROTO, false>), dim3(g), dim3(PB_WG), K->lds_pad, st, *K);
+    }
+    else if (K->xs_grid && K->xp)
     {
         const size_t lds = (size_t)K->xs_np * PB_XREG + K->lds_pad;
         const bool w512 = K->xp_wgt == 512;
@@ -2218,7 +2617,27 @@ static void pbk_launch_small(const pb_kargs *K, uint32_t grid, hipStream_t st)
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
 {
-    if (K->fst_g)
+    if (K->vl)
+    {
+        const uint32_t grid = (uint32_t)((K->n_frames + K->vl_wgf - 1) / K->vl_wgf);
+        const size_t lds = PB_VL_LDS(K->vl_wgf, K->hl == 54 ? 5 : 4, K->vl_nl48, K->vl_nlines) + K->lds_pad;
+        const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
+        if (K->hl == 54)
+        {
+            if (l4)
+                hipLaunchKernelGGL((pb_vline_kernel<54, true>), dim3(grid), dim3(PB_WG), lds, st, *K);
+            else
+                hipLaunchKernelGGL((pb_vline_kernel<54, false>), dim3(grid), dim3(PB_WG), lds, st, *K);
+        }
+        else
+        {
+            if (l4)
+                hipLaunchKernelGGL((pb_vline_kernel<42, true>), dim3(grid), dim3(PB_WG), lds, st, *K);
+            else
+                hipLaunchKernelGGL((pb_vline_kernel<42, false>), dim3(grid), dim3(PB_WG), lds, st, *K);
+        }
+    }
+    else if (K->fst_g)
     {
         const uint32_t grid = (uint32_t)((K->n_frames + K->fst_wgf - 1) / K->fst_wgf);
         const size_t lds = (size_t)K->fst_nbuf * K->fst_sb + PB_FST_LDS(K->fst_wgf) + K->lds_pad;
@@ -2374,10 +2793,10 @@ __global__ __launch_bounds__(256) void pb_len_wgsum(pb_kargs K, uint32_t wgf, ui
         l2[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
-extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t *bsum, uint32_t nblk, unsigned long long *l2,
-                                             uint32_t n_l2, uint64_t *offsets, hipStream_t st)
+extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t wgf, uint32_t *bsum, uint32_t nblk,
+                                             unsigned long long *l2, uint32_t n_l2, uint64_t *offsets, hipStream_t st)
 {
-    hipLaunchKernelGGL(pb_len_wgsum, dim3(n_l2), dim3(256), 0, st, *K, K->stage_wgf, nblk, bsum, l2);
+    hipLaunchKernelGGL(pb_len_wgsum, dim3(n_l2), dim3(256), 0, st, *K, wgf, nblk, bsum, l2);
     hipLaunchKernelGGL(pb_scan_blocks, dim3(1), dim3(1024), 0, st, l2, n_l2, offsets, K->n_frames);
     return hipGetLastError();
 }

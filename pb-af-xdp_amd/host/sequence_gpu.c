@@ -27,8 +27,15 @@
 #include <unistd.h>
 
 #define PB_MAX_WORKERS 1024
-#define PB_LAND_INFLIGHT 3 /* landings queued per thread */
-#define PB_LAND_CHUNK 1024 /* frames per landing (a quarter of the UMEM) */
+#define PB_LAND_INFLIGHT_MAX 16 /* landings queued per thread (PB_LAND_INFLIGHT, default 3) */
+#define PB_LAND_CHUNK_DEF 1024   /* frames per landing (PB_LAND_CHUNK; a quarter of the UMEM) */
+
+static uint32_t env_u32(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi)
+{
+    const char *e = getenv(name);
+    long v = e ? atol(e) : (long)dflt;
+    return v < (long)lo ? lo : (v > (long)hi ? hi : (uint32_t)v);
+}
 #define PB_BATCH_BYTES_MAX (256ull << 20) /* device bytes per frame buffer (two per worker) */
 
 static uint64_t total_pckts[PB_MAX_SEQUENCES];
@@ -440,6 +447,10 @@ static void *gpu_worker(void *p)
      * without it one landed chunk is one submit */
     xsk.batch = w->cmd.batch_set ? w->cmd.batch_size : 0u;
 
+    /* landing granularity: frames per landing and landings in flight (their launch and
+     * completion latencies overlap); tunable for the host-rate probe (scripts/e2e_probe.py) */
+    const uint32_t land_chunk = env_u32("PB_LAND_CHUNK", PB_LAND_CHUNK_DEF, 1, nslots);
+    const uint32_t land_inflight = env_u32("PB_LAND_INFLIGHT", 3, 1, PB_LAND_INFLIGHT_MAX);
     const double t0 = now_s();
     uint64_t my_frames = 0; /* this thread's frames: the delay pacing (per thread) */
     uint64_t step = 0;
@@ -470,11 +481,11 @@ static void *gpu_worker(void *p)
          * c + 1 lands while chunk c is submitted (their latencies overlap) */
         uint64_t f0 = 0, f_issue = 0;
         uint32_t land_slot = xsk.next_slot, in_land = 0;
-        uint32_t qn_[PB_LAND_INFLIGHT];
+        uint32_t qn_[PB_LAND_INFLIGHT_MAX];
         int qh = 0, qn = 0;
         while (f0 < nf && !done && !stop_requested)
         {
-            while (qn < PB_LAND_INFLIGHT && f_issue < nf)
+            while (qn < (int)land_inflight && f_issue < nf)
             {
                 uint32_t free_slots = pb_xsk_free_slots(&xsk) - in_land;
                 if (free_slots == 0)
@@ -487,7 +498,7 @@ static void *gpu_worker(void *p)
                         break;
                     continue;
                 }
-                uint32_t n = free_slots < PB_LAND_CHUNK ? free_slots : PB_LAND_CHUNK;
+                uint32_t n = free_slots < land_chunk ? free_slots : land_chunk;
                 if ((uint64_t)n > nf - f_issue)
                     n = (uint32_t)(nf - f_issue);
                 if (n > nslots - land_slot) /* the slot ring wraps: a chunk never does */
@@ -500,7 +511,7 @@ static void *gpu_worker(void *p)
                     done = 3;
                     break;
                 }
-                qn_[(qh + qn) % PB_LAND_INFLIGHT] = n;
+                qn_[(qh + qn) % land_inflight] = n;
                 ++qn;
                 in_land += n;
                 land_slot = (land_slot + n) & (nslots - 1);
@@ -516,7 +527,7 @@ static void *gpu_worker(void *p)
                 break;
             }
             uint32_t n = qn_[qh];
-            qh = (qh + 1) % PB_LAND_INFLIGHT;
+            qh = (qh + 1) % land_inflight;
             --qn;
             in_land -= n;
             const uint16_t *ln = lens + xsk.next_slot;

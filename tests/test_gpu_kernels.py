@@ -19,12 +19,13 @@ pytestmark = pytest.mark.gpu
 SHAPES = [
     ("gpf", {"PBGPU_KERNEL": "gpf"}, ("pb_gpf_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("nopage_small", {"PBGPU_KERNEL": "nopage"},
-     ("pb_small_kernel", "pb_xsmall_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel")),
+     ("pb_small_kernel", "pb_xsmall_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel",
+      "pb_vline_kernel")),
     ("xpage_forced", {"PBGPU_XP_FORCE": "1"},
      ("pb_xpage_kernel", "pb_xsmall_kernel", "pb_small_kernel<", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel",
-      "pb_vstage_kernel")),
+      "pb_vstage_kernel", "pb_vline_kernel")),
     ("linear_small", {"PBGPU_KERNEL": "linear"},
-     ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel")),
+     ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel", "pb_vline_kernel")),
     ("stage_g8_wgf5", {"PBGPU_KERNEL": "stage", "PBGPU_G": "8", "PBGPU_WGF": "5"},
      ("pb_stage_kernel<8", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("stage_g64_kb4", {"PBGPU_KERNEL": "stage", "PBGPU_G": "64", "PBGPU_STAGE_KB": "4"},
@@ -35,29 +36,29 @@ SHAPES = [
      ("pb_stage_kernel<32", "pb_xsmall_kernel", "pb_small_kernel<")),
     # pb_vstage_kernel (random payloads) at other lane-group / window / workgroup sizes;
     # static and mixed payloads keep pb_stage_kernel at the same shape
-    ("vstage_g16", {"PBGPU_G": "16"},
+    ("vstage_g16", {"PBGPU_G": "16", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<16", "pb_stage_kernel<16", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
-    ("vstage_g64_kb8", {"PBGPU_G": "64", "PBGPU_STAGE_KB": "8"},
+    ("vstage_g64_kb8", {"PBGPU_G": "64", "PBGPU_STAGE_KB": "8", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<64", "pb_stage_kernel<64", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
-    ("vstage_g32_wgf7", {"PBGPU_G": "32", "PBGPU_WGF": "7"},
+    ("vstage_g32_wgf7", {"PBGPU_G": "32", "PBGPU_WGF": "7", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<32", "pb_stage_kernel<32", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
     # pb_vstage_kernel's lane layouts by window: fixed 8-lane groups (bit 4) and
     # no 32-lane groups (bit 5) build the same bytes as the default 32/16/8 layout
-    ("vstage_fixed8", {"PBGPU_FST_DBG": "16"},
+    ("vstage_fixed8", {"PBGPU_FST_DBG": "16", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
-    ("vstage_no32", {"PBGPU_FST_DBG": "32"},
+    ("vstage_no32", {"PBGPU_FST_DBG": "32", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
     # the other correct-output switches: workgroup edges at frame starts (lines split between
     # workgroups, masked stores at every edge), natural window order, the 3-pass offsets scan
-    ("vstage_split_edges", {"PBGPU_FST_DBG": "64"},
+    ("vstage_split_edges", {"PBGPU_FST_DBG": "64", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
-    ("vstage_no_order", {"PBGPU_FST_DBG": "256"},
+    ("vstage_no_order", {"PBGPU_FST_DBG": "256", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
-    ("vstage_3pass_kb8", {"PBGPU_VST_SCAN": "3pass", "PBGPU_STAGE_KB": "8"},
+    ("vstage_3pass_kb8", {"PBGPU_VST_SCAN": "3pass", "PBGPU_STAGE_KB": "8", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
 ]
@@ -147,8 +148,9 @@ XS_LENS = [42, 43, 44, 48, 52, 56, 60, 64, 72, 96, 98, 100, 106, 108, 116, 120, 
 XS_COUNTS = [1, 5, 200, 2048, 2049, 2 * 2048 * 5 + 77]
 
 
-@pytest.mark.parametrize("force_xpage", [False, True, 512, "lin64", "lin128"],
-                         ids=["default", "xpage_forced", "xpage_forced_512", "linear_wg64", "linear_wg128"])
+@pytest.mark.parametrize("force_xpage", [False, True, 512, "lin64", "lin128", "win1", "win4"],
+                         ids=["default", "xpage_forced", "xpage_forced_512", "linear_wg64", "linear_wg128",
+                              "windows_1", "windows_4"])
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
 @pytest.mark.parametrize("flen", XS_LENS)
 def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
@@ -161,6 +163,11 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
         monkeypatch.delenv("PBGPU_XP_FORCE", raising=False)
         monkeypatch.setenv("PBGPU_KERNEL", "linear")
         monkeypatch.setenv("PBGPU_SMALL_WGT", force_xpage[3:])
+    win = force_xpage in ("win1", "win4")
+    if win:  # the windowed small kernel (pb_swin_kernel) for every length
+        monkeypatch.delenv("PBGPU_XP_FORCE", raising=False)
+        monkeypatch.setenv("PBGPU_KERNEL", "linear")
+        monkeypatch.setenv("PBGPU_SMALL_WIN", force_xpage[3:])
     hl = 54 if proto == "tcp" else 42
     if flen < hl or (proto == "icmp" and flen == hl):
         pytest.skip("shorter than the headers / empty static payload")
@@ -173,7 +180,9 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
         n = max(1, n * 64 // flen)  # page counts as named above at every length
         kern = _check(ctx, cfg, 1000003 + n, n)
         xp_default = flen <= 64 and 512 // ((4096 + flen - 1) // flen + 1) >= 6
-        if lin:
+        if win:
+            want = "pb_swin_kernel<"
+        elif lin:
             want = "pb_small_kernel<"
         elif flen % 4 == 0 and (force_xpage or (4096 % flen and xp_default)):
             want = "pb_xpage_kernel"
@@ -261,9 +270,10 @@ def test_vstage_fixed_odd_lengths(ctx, proto, flen):
 
 @pytest.mark.parametrize("lo,hi", [(0, 1), (0, 5), (0, 40), (60, 1500), (1400, 1500), (0, 3000)])
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
-def test_vstage_variable_lengths(ctx, proto, lo, hi):
+def test_vstage_variable_lengths(ctx, monkeypatch, proto, lo, hi):
     """Packed variable frames from header-only (frames sharing chunks on both
     sides, empty payloads) to 3 KB."""
+    monkeypatch.setenv("PBGPU_KERNEL", "vstage")
     hl = 54 if proto == "tcp" else 42
     cfg = _fst_cfg(proto, hl + 100)
     cfg["payloads"] = [{"length": {"min": lo, "max": hi}}]
@@ -278,11 +288,64 @@ def test_vstage_variable_lengths(ctx, proto, lo, hi):
     [{"length": {"min": 0, "max": 3}}, {"length": {"min": 7, "max": 7}}, {"length": {"min": 500, "max": 1400}}],
 ], ids=["two_var", "two_fixed_1500", "three_mixed_lengths"])
 @pytest.mark.parametrize("proto", ["udp", "tcp"])
-def test_multi_random_payloads(ctx, proto, pls):
+@pytest.mark.parametrize("kernel", ["default", "vstage"])
+def test_multi_random_payloads(ctx, monkeypatch, proto, pls, kernel):
     """Several random payloads per iteration (one frame each, later payloads drawn
     from the advanced seed, sequence.c:529-561): packed variable frames through
-    pb_vstage_kernel, bit-exact against the oracle."""
+    pb_vline_kernel (every payload >= 32 B) or pb_vstage_kernel, bit-exact against
+    the oracle."""
+    if kernel == "vstage":
+        monkeypatch.setenv("PBGPU_KERNEL", "vstage")
     cfg = _fst_cfg(proto, 200)
     cfg["payloads"] = pls
     kern = _check(ctx, cfg, 31, 1500)
-    assert kern.startswith("pb_vstage_kernel<"), kern
+    vl = kernel == "default" and min(p["length"]["min"] for p in pls) >= 32
+    assert kern.startswith("pb_vline_kernel<" if vl else "pb_vstage_kernel<"), kern
+
+
+# pb_vline_kernel: packed variable frames with payloads of >= 32 B (two frame starts in one
+# 128-B line at 32-40 B), up to 4096-B frames, every protocol, with and without the L4
+# checksum; frame counts that leave ragged workgroups and single-frame launches
+VL_RANGES = [(32, 33), (32, 40), (32, 200), (60, 1500), (64, 1500), (1400, 1500), (500, 4000), (3000, 4042)]
+
+
+@pytest.mark.parametrize("lo,hi", VL_RANGES)
+@pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
+@pytest.mark.parametrize("csum", [True, False])
+def test_vline_variable_lengths(ctx, proto, lo, hi, csum):
+    hl = 54 if proto == "tcp" else 42
+    cfg = _fst_cfg(proto, hl + 100, csum)
+    cfg["payloads"] = [{"length": {"min": lo, "max": hi}}]
+    big = max(300, min(40000, (24 << 20) // (hl + hi)))
+    for first, n in ((5, 1), (0, 3), (11, 253), (2 ** 40 + 7, 1000), (1, big)):
+        kern = _check(ctx, cfg, first, n)
+        assert kern.startswith("pb_vline_kernel<%d, %d>" % (hl, int(csum))), kern
+
+
+@pytest.mark.parametrize("wgf", ["32", "100", "252"])
+def test_vline_workgroup_sizes(ctx, monkeypatch, wgf):
+    """Own frames per workgroup (PBGPU_VL_WGF): every region split and ghost count."""
+    monkeypatch.setenv("PBGPU_VL_WGF", wgf)
+    for lo, hi in ((32, 33), (64, 1500)):
+        cfg = pc.get("c3_udp_var")
+        cfg["payloads"] = [{"length": {"min": lo, "max": hi}}]
+        kern = _check(ctx, cfg, 77, 20011)
+        assert kern.startswith("pb_vline_kernel<"), kern
+
+
+def test_vline_matches_vstage_at_size(ctx, monkeypatch):
+    """configs[2] at 2^22 frames: the two variable-length kernels build the same bytes."""
+    seq = Sequence.from_config(pc.get("c3_udp_var"))
+    out = {}
+    for kernel in ("vline", "vstage"):
+        if kernel == "vstage":
+            monkeypatch.setenv("PBGPU_KERNEL", "vstage")
+        ctx.load_sequence(6, seq, pc.SEED_BASE)
+        fb = ctx.alloc_frames(*ctx.build_size(6, 1 << 22))
+        ctx.build(6, 3 << 30, 1 << 22, fb)
+        ctx.sync()
+        out[kernel] = (fb.packed(), fb.offsets(), ctx.kernel_name(6))
+        fb.free()
+    assert out["vline"][2].startswith("pb_vline_kernel") and out["vstage"][2].startswith("pb_vstage_kernel")
+    assert np.array_equal(out["vline"][1], out["vstage"][1])
+    assert np.array_equal(out["vline"][0], out["vstage"][0])
