@@ -164,7 +164,7 @@ int pbgpu_kernel_times(pbgpu_ctx *ctx, double *ms_each, uint32_t cap, uint32_t *
  * fills).  pbgpu_fill_probe returns the fastest shape's mean
  * device time per launch; _ex returns every shape's and the fastest's index,
  * pbgpu_fill_shape_name names a shape. */
-#define PBGPU_FILL_SHAPES 12
+#define PBGPU_FILL_SHAPES 15
 int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_launch);
 int pbgpu_fill_probe_ex(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_shape, int *best_shape);
 const char *pbgpu_fill_shape_name(int shape);

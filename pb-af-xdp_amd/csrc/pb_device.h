@@ -21,7 +21,7 @@
 #define PB_LCG48_N 4200                    // lcg48[m] = L^(48 m), m < 4200 (> 16-B chunks of a 64 KiB frame)
 #define PB_XPG 4096                        // XCD-owned page bytes (pb_xsmall_kernel, pb_xpage_kernel)
 #define PB_XREG (PB_XPG + 256)             // LDS bytes per page region (128 B slack either side)
-#define PBK_FILL_SHAPES 12                 // write-roofline probe shapes (pbk_launch_fill)
+#define PBK_FILL_SHAPES 15                 // write-roofline probe shapes (pbk_launch_fill)
 #define PB_XNP_MAX 8                       // pb_xsmall_kernel: pages per workgroup, 4 (64-B frames) or 8 (128-B)
 #define PB_CTR_SHARDS 64                   // per-sequence counter shards (workgroup b adds to shard b % 64)
 #define PB_CTR_STRIDE 16                   // u64 words per shard: one 128-B line each ({frames, bytes} + pad)
@@ -142,7 +142,7 @@ struct pb_kargs
     const uint32_t *lit_stop;
     uint32_t small_wgt;     // pb_small_kernel's threads (= frames) per workgroup: 256 (0), 128 or 64
     // pb_vline_kernel (packed variable lengths, every payload random, stream rule)
-    const uint32_t *orbit;  // LCG-orbit prefix sums: orbit[t] = {PE(8t), PO(8t)} mod 0xFFFF (u16 pair), t <= 2^21
+    const uint32_t *orbit;  // LCG-orbit prefix sums: orbit[t] = {PE(t << PB_ORB_SH), PO(..)} mod 0xFFFF (u16 pair)
     uint32_t orbit_tot;     // PE(2^24) mod 0xFFFF (= PO(2^24)): runs that wrap the orbit
     uint32_t vl;            // 1: launch pb_vline_kernel
     uint32_t vl_wgf;        // its own frames per workgroup (<= 256 - PB_VST_GHOSTS)
@@ -177,6 +177,7 @@ struct pb_kargs
 // record and nsp 16-B header chunks, a zero chunk and 17 chunk masks, the lcg48 entries, the
 // line map (u16)
 #define PB_VL_STEP 16384u // bytes of a workgroup's region per step (4 waves x 4 KiB)
+#define PB_ORB_SH 5       // orbit prefix sums sampled every 2^PB_ORB_SH positions (2 MiB table)
 #define PB_VL_LDS(wgf, nsp, nl48, nlines)                                                                     \
     ((size_t)256 + ((size_t)(wgf) + PB_VST_GHOSTS) * 16 * (1 + (size_t)(nsp)) + 18 * 16 + (size_t)(nl48) * 8 + \
      (((size_t)(nlines) + 7) & ~(size_t)7) * 2)

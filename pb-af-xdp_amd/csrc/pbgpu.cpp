@@ -237,17 +237,18 @@ std::vector<uint2> make_jump_table()
 
 // pb_vline_kernel's payload sums (pbgpu_kernels.hip, pb_orbit_sum): M = L^3 mod 2^24 walks one
 // orbit of all 2^24 states from 0 (full period: c odd, a = 1 mod 4); entry t holds the sums of
-// the bytes (bits 16-23) at the even and the odd positions before 8t, mod 0xFFFF, as two u16.
+// the bytes (bits 16-23) at the even and the odd positions before t << PB_ORB_SH, mod 0xFFFF,
+// as two u16.
 std::vector<uint32_t> make_orbit_table(uint32_t *total)
 {
     const uint32_t m = 0xFFFFFFu;
     const uint32_t a3 = (PB_LCG_A * PB_LCG_A * PB_LCG_A) & m, c3 = (PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u)) & m;
-    std::vector<uint32_t> t((1u << 21) + 1);
+    std::vector<uint32_t> t((1u << (24 - PB_ORB_SH)) + 1);
     uint32_t y = 0, pe = 0, po = 0;
     for (uint32_t k = 0; k < (1u << 24); ++k)
     {
-        if ((k & 7u) == 0)
-            t[k >> 3] = pe | (po << 16);
+        if ((k & ((1u << PB_ORB_SH) - 1u)) == 0)
+            t[k >> PB_ORB_SH] = pe | (po << 16);
         const uint32_t b = (y >> 16) & 0xFFu;
         if (k & 1u)
             po = (po + b) % 0xFFFFu;
@@ -255,7 +256,7 @@ std::vector<uint32_t> make_orbit_table(uint32_t *total)
             pe = (pe + b) % 0xFFFFu;
         y = (a3 * y + c3) & m;
     }
-    t[1u << 21] = pe | (po << 16);
+    t[1u << (24 - PB_ORB_SH)] = pe | (po << 16);
     *total = pe; // the even and odd totals are equal (each byte value 2^15 times per parity)
     return t;
 }

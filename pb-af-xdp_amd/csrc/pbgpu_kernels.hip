@@ -2076,8 +2076,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
 // The L4 payload sum: payload byte j is bits 16-23 of M^(j+1)(st0), M = L^3 mod 2^24 (full
 // period), so a payload is a run of consecutive orbit positions [p, p + n) of M, p = the discrete
 // log of M(st0) (24 fixed steps, the PCG "distance" construction), and its word sum is a
-// difference of prefix sums of the orbit's even- and odd-position bytes (K.orbit, every 8th
-// position, <= 7 LCG steps at each end).
+// difference of prefix sums of the orbit's even- and odd-position bytes (K.orbit, every 32nd
+// position: a 2-MiB table that stays in the XCD's L2, <= 31 LCG steps at each end; every 8th
+// position, an 8-MiB table, read 7 GB per configs[2] launch through the fabric).
 
 // discrete-log constants: M^(2^i) as (a_i, c_i) mod 2^24
 constexpr uint32_t PB_M24 = 0xFFFFFFu;
@@ -2121,26 +2122,22 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     uint32_t q = p + n, wrap = 0;
     if (q >= (1u << 24)) // the run wraps the orbit (2^24 is even: parities keep)
         q -= 1u << 24, wrap = K.orbit_tot;
-    const uint32_t tp = K.orbit[(p + 7) >> 3], tq = K.orbit[(q + 7) >> 3];
-    // prefix sums at p and q from the next sampled position, minus the bytes in between
-    uint32_t e_p = 0, o_p = 0, e_q = 0, o_q = 0;
+    constexpr uint32_t SM = (1u << PB_ORB_SH) - 1u;
+    const uint32_t tp = K.orbit[(p + SM) >> PB_ORB_SH], tq = K.orbit[(q + SM) >> PB_ORB_SH];
+    // prefix sums at p and q from the next sampled position, minus the bytes in between (walked
+    // with the LCG; a[t & 1] collects the bytes at positions p + t of one parity)
+    uint32_t ap[2] = {0u, 0u}, aq[2] = {0u, 0u};
     uint32_t y = yp, z = yq;
-    const uint32_t cp = (8u - (p & 7u)) & 7u, cq = (8u - (q & 7u)) & 7u;
+    const uint32_t cp = (SM + 1u - (p & SM)) & SM, cq = (SM + 1u - (q & SM)) & SM;
 #pragma unroll
-    for (uint32_t t = 0; t < 7; ++t)
+    for (uint32_t t = 0; t < SM; ++t)
     {
-        const uint32_t bp = t < cp ? (y >> 16) & 0xFFu : 0u, bq = t < cq ? (z >> 16) & 0xFFu : 0u;
-        if ((p + t) & 1u)
-            o_p += bp;
-        else
-            e_p += bp;
-        if ((q + t) & 1u)
-            o_q += bq;
-        else
-            e_q += bq;
+        ap[t & 1u] += t < cp ? (y >> 16) & 0xFFu : 0u;
+        aq[t & 1u] += t < cq ? (z >> 16) & 0xFFu : 0u;
         y = __umul24(y, PB_A3) + PB_C3;
         z = __umul24(z, PB_A3) + PB_C3;
     }
+    const uint32_t e_p = ap[p & 1u], o_p = ap[(p & 1u) ^ 1u], e_q = aq[q & 1u], o_q = aq[(q & 1u) ^ 1u];
     // PE(q) - PE(p), PO(q) - PO(p), kept positive with multiples of 0xFFFF
     const uint32_t de = (tq & 0xFFFFu) + wrap + e_p + 2u * 0xFFFFu - e_q - (tp & 0xFFFFu);
     const uint32_t dO = (tq >> 16) + wrap + o_p + 2u * 0xFFFFu - o_q - (tp >> 16);
@@ -2275,7 +2272,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         const uint32_t r = (uint32_t)(start - wbase);
         const uint32_t s0 = r & 15u;
         const uint2 jt = s_jt[s0];
-        s_rec[tix] = pb_u32x4{r, r + flen, jt.x * st0 + jt.y, 0u};
+        s_rec[tix] = pb_u32x4{r >> 4, r + HL, r + flen, jt.x * st0 + jt.y};
         // the header image shifted to byte s0 of the frame's first chunk: out dword u holds image
         // bytes [4u - s0, 4u - s0 + 4)
         const uint32_t q = s0 >> 2, sh = s0 & 3u;
@@ -2314,72 +2311,73 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         const pb_u32x4 rc = s_rec[tix];
         // lines whose first byte lies in this frame: the frame holding it, and where (if at all)
         // the next frame starts in the line
-        const uint32_t a = rc[0] > lo_rel ? rc[0] - lo_rel : 0u, b = rc[1] > lo_rel ? rc[1] - lo_rel : 0u;
+        const uint32_t st = rc[1] - HL;
+        const uint32_t a = st > lo_rel ? st - lo_rel : 0u, b = rc[2] > lo_rel ? rc[2] - lo_rel : 0u;
         const uint32_t la = (a + 127u) >> 7, lb = min((b + 127u) >> 7, nlines);
-        // the next two frames' starts in the line as 16-B chunk positions ceil(o / 16) (1..8; 15:
-        // none): a chunk k of the line lies in frame tix + (k >= c1) + (k >= c2)
-        const uint32_t b2 = (uint32_t)tix + 1u < nfr ? s_rec[tix + 1][1] - lo_rel : 0xFFFFFFFFu;
+        // the next two frames' starts in the line as 16-B chunk positions c = ceil(o / 16) (1..8,
+        // 8: none), kept as 8 - c in bits 0-2 and 4-6: chunk k of the line lies in frame
+        // tix + (k >= c1) + (k >= c2), and k >= c <=> k + (8 - c) carries into bit 3 / 7
+        const uint32_t b2 = (uint32_t)tix + 1u < nfr ? s_rec[tix + 1][2] - lo_rel : 0xFFFFFFFFu;
         for (uint32_t L = la; L < lb; ++L)
         {
             const uint32_t o1 = b - (L << 7), o2 = b2 - (L << 7);
-            const uint32_t c1 = o1 < 128u ? (o1 + 15u) >> 4 : 15u, c2 = o2 < 128u ? (o2 + 15u) >> 4 : 15u;
-            s_map[L] = (uint16_t)((uint32_t)tix | (c1 << 8) | (c2 << 12));
+            const uint32_t c1 = o1 < 128u ? (o1 + 15u) >> 4 : 8u, c2 = o2 < 128u ? (o2 + 15u) >> 4 : 8u;
+            s_map[L] = (uint16_t)(((uint32_t)tix << 8) | (8u - c1) | ((8u - c2) << 4));
         }
     }
     if (tid <= 16u) // chunk byte masks: s_m16[k] keeps bytes >= k
         s_m16[tid] = pb_u32x4{pb_range_mask((int)tid, 4), pb_range_mask((int)tid - 4, 4), pb_range_mask((int)tid - 8, 4),
                               pb_range_mask((int)tid - 12, 4)};
-    if (tid == 32u)
-        s_img[CAP * NSP] = pb_u32x4{0u, 0u, 0u, 0u}; // the zero header chunk
+    if (tid == 32u) // the header chunk after the last record's: no frame starts there
+        s_img[nfr * NSP] = pb_u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
 
     // ---------------- stream: the region in 16-KiB steps, no barriers ----------------
-    // Chunk at region offset c (absolute pos = lo + c): frame f holds its first byte, g = f + 1
-    // may start inside it.  Its bytes = f's payload bytes in [max(S_f + HL, pos), min(E_f, pos + 16))
-    // (one generated chunk, masked) | f's header bytes if the chunk is one of f's first NSP (the
-    // shifted image) | g's header bytes if g starts inside the chunk (g's first image chunk):
-    // one straight-line path for every chunk, and every 128-B line leaves in one store instruction.
-    const uint32_t zero = CAP * NSP;
-    uint8_t *const gout = K.out + wbase;
+    // Chunk ci (16-B units from wbase) of line l: frame f holds its first byte, and its bytes are
+    // f's payload bytes in [plo, phi) (one generated chunk, masked) and header bytes elsewhere:
+    // f's own (chunk m < NSP of f: the shifted image, bytes < plo) or the next frame's, which
+    // starts inside the chunk when phi < 16 (then m >= NSP, and image slot f * NSP + NSP is the
+    // next frame's first chunk, bytes >= phi; for a chunk with neither both masks are empty).
+    // One straight-line path per chunk, and every 128-B line leaves in one store instruction.
+    uint8_t *const gout = K.out + wbase + lo_rel;
     const bool store = !(K.fst_dbg & 2u);
     const uint32_t nsteps = (R + PB_VL_STEP - 1u) / PB_VL_STEP;
+    const uint32_t k = lane & 7u, kk = k | (k << 4), ck = (lo_rel >> 4) + k;
+    const uint32_t lmax = nlines ? nlines - 1u : 0u;
     for (uint32_t s = 0; s < nsteps; ++s)
     {
         // four independent chunks per lane, computed before any is stored (straight-line: their
-        // LDS reads and LCG chains overlap); chunks past the region's end are computed on chunk 0
-        // and not stored
+        // LDS reads and LCG chains overlap); lines past the region's end are computed on its last
+        // line and not stored
         pb_u32x4 v[4];
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
         {
-            const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
-            const uint32_t c = c0 < R ? c0 : 0u;
-            const uint32_t pos = lo_rel + c;
-            const uint32_t e = s_map[c >> 7], k = (c >> 4) & 7u;
-            const uint32_t f = (e & 0xFFu) + (k >= ((e >> 8) & 15u) ? 1u : 0u) + (k >= (e >> 12) ? 1u : 0u);
+            const uint32_t l = min(s * (PB_VL_STEP / 128u) + (wv << 5) + (i << 3) + (lane >> 3), lmax);
+            const uint32_t ci = (l << 3) + ck;
+            const uint32_t t = (uint32_t)s_map[l] + kk;
+            const uint32_t f = (t >> 8) + __popc(t & 0x88u);
             const pb_u32x4 rc = s_rec[f];
-            const uint32_t cb = rc[0] & ~15u;
-            const uint32_t m = (pos - cb) >> 4; // chunk index within frame f
+            const uint32_t m = ci - rc[0]; // chunk index within frame f
             const uint2 L = s_l48[m];
-            const uint32_t x = __umul24(rc[2], L.x) + L.y;
-            const uint32_t plo = rc[0] + HL > pos ? min(rc[0] + HL - pos, 16u) : 0u;
-            const uint32_t phi = min(rc[1] - pos, 16u);
-            const bool g_in = phi < 16u && f + 1u < nfr; // the next frame starts inside the chunk
-            const pb_u32x4 ha = s_img[m < NSP ? f * NSP + m : zero];
-            const pb_u32x4 hb = s_img[g_in ? (f + 1u) * NSP : zero];
+            const uint32_t x = __umul24(rc[3], L.x) + L.y;
+            const int32_t pb = (int32_t)(ci << 4);
+            const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
+            const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
+            const pb_u32x4 h = s_img[f * NSP + min(m, NSP)];
             const pb_u32x4 ml = s_m16[plo], mh = s_m16[phi];
-            uint32_t o0 = x, o1 = x, o2 = x, o3 = x;
-            if (!(K.fst_dbg & 1u)) // (PBGPU_FST_DBG bit 0, diagnostics only: no payload generation)
-                pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
-            v[i] = pb_u32x4{(o0 & ml[0] & ~mh[0]) | ha[0] | hb[0], (o1 & ml[1] & ~mh[1]) | ha[1] | hb[1],
-                            (o2 & ml[2] & ~mh[2]) | ha[2] | hb[2], (o3 & ml[3] & ~mh[3]) | ha[3] | hb[3]};
+            uint32_t o0, o1, o2, o3;
+            pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+            const uint32_t M0 = ml[0] & ~mh[0], M1 = ml[1] & ~mh[1], M2 = ml[2] & ~mh[2], M3 = ml[3] & ~mh[3];
+            v[i] = pb_u32x4{(o0 & M0) | (h[0] & ~M0), (o1 & M1) | (h[1] & ~M1), (o2 & M2) | (h[2] & ~M2),
+                            (o3 & M3) | (h[3] & ~M3)};
         }
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
         {
             const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
             if (store && c0 < R)
-                pb_st16(gout + lo_rel + c0, v[i]);
+                pb_st16(gout + c0, v[i]);
         }
     }
     if (tid == 0) // the workgroup stores exactly [lo, hi) (the launch's last chunk zero-padded)
@@ -2539,6 +2537,26 @@ __global__ __launch_bounds__(256) void pb_fill_kernel(pb_u32x4 *dst, uint64_t n1
             if (NT)
                 __builtin_nontemporal_store(pb_u32x4{v, v ^ (uint32_t)c, v, (uint32_t)c}, dst + c);
             else
+                dst[c] = pb_u32x4{v, v ^ (uint32_t)c, v, (uint32_t)c};
+        }
+    }
+}
+
+// write-only probe of pb_vline_kernel's store shape: each workgroup owns a contiguous region of
+// RB KiB (XCD-contiguous regions) and writes it in 16-KiB steps, wave w the 4-KiB quarter w of a
+// step as four 1-KiB store instructions
+template <int RB>
+__global__ __launch_bounds__(256) void pb_fillreg_kernel(pb_u32x4 *dst, uint64_t n16, uint32_t v)
+{
+    const uint64_t b = (uint64_t)pb_xcd_region(blockIdx.x, gridDim.x) * (RB * 64);
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (uint32_t s = 0; s < RB / 16; ++s)
+    {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+        {
+            const uint64_t c = b + s * 1024u + wv * 256u + i * 64u + lane;
+            if (c < n16)
                 dst[c] = pb_u32x4{v, v ^ (uint32_t)c, v, (uint32_t)c};
         }
     }
@@ -2846,13 +2864,17 @@ __global__ __launch_bounds__(512) void pb_fill512_kernel(pb_u32x4 *dst, uint64_t
 //  8  hipMemsetD32Async (the runtime's fill)
 //  9-11  shapes 0, 2 and 5 with XCD-contiguous regions (each XCD fills its own eighth, as the
 //        staged build kernels write since pb_xcd_region)
+//  12-14 pb_vline_kernel's shape: a 208 / 64 / 16-KiB region per workgroup in 16-KiB steps,
+//        5 workgroups / CU, XCD-contiguous
 extern "C" const char *pbk_fill_shape_name(int mode)
 {
     static const char *names[PBK_FILL_SHAPES] = {
         "16KiB/wg 4 st/lane", "16KiB/wg 4 st/lane nt", "4KiB/wg 1 st/lane (8 wg/CU)", "4KiB/wg 1 st/lane, 6 wg/CU",
         "4KiB/wg 1 st/lane, 5 wg/CU", "4KiB/wg 1 st/lane, 4 wg/CU", "4KiB/wg 1 st/lane, 3 wg/CU",
         "8KiB/512-thread wg 1 st/lane", "hipMemsetD32Async", "16KiB/wg 4 st/lane, XCD-contiguous",
-        "4KiB/wg 1 st/lane (8 wg/CU), XCD-contiguous", "4KiB/wg 1 st/lane, 4 wg/CU, XCD-contiguous"};
+        "4KiB/wg 1 st/lane (8 wg/CU), XCD-contiguous", "4KiB/wg 1 st/lane, 4 wg/CU, XCD-contiguous",
+        "208KiB region/wg 16KiB steps, 5 wg/CU", "64KiB region/wg 16KiB steps, 5 wg/CU",
+        "16KiB region/wg, 5 wg/CU"};
     return mode >= 0 && mode < PBK_FILL_SHAPES ? names[mode] : "?";
 }
 
@@ -2889,6 +2911,18 @@ extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipSt
     case 11:
         hipLaunchKernelGGL((pb_fill_kernel<false, 1, true>), dim3(g1), dim3(256), mode == 10 ? 0u : cap_lds[2], st,
                            (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+        break;
+    case 12:
+        hipLaunchKernelGGL((pb_fillreg_kernel<208>), dim3((uint32_t)((n16 + 208 * 64 - 1) / (208 * 64))), dim3(256),
+                           cap_lds[1], st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+        break;
+    case 13:
+        hipLaunchKernelGGL((pb_fillreg_kernel<64>), dim3((uint32_t)((n16 + 64 * 64 - 1) / (64 * 64))), dim3(256),
+                           cap_lds[1], st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
+        break;
+    case 14:
+        hipLaunchKernelGGL((pb_fillreg_kernel<16>), dim3((uint32_t)((n16 + 16 * 64 - 1) / (16 * 64))), dim3(256),
+                           cap_lds[1], st, (pb_u32x4 *)dst, n16, 0x5A5A5A5Au);
         break;
     default:
         return hipMemsetD32Async((hipDeviceptr_t)dst, 0x5A5A5A5Au, bytes / 4, st);

@@ -434,7 +434,7 @@ class GpuContext:
         _check(self.lib.pbgpu_fill_probe(self.h, nbytes, reps, C.byref(ms)), "fill_probe")
         return float(ms.value)
 
-    FILL_SHAPES = 12  # PBGPU_FILL_SHAPES
+    FILL_SHAPES = 15  # PBGPU_FILL_SHAPES
 
     def fill_probe_shapes(self, nbytes: int, reps: int):
         """Every write-probe shape's mean ms per launch {name: ms} and the fastest's name."""
