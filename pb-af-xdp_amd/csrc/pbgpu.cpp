@@ -136,7 +136,7 @@ struct pbgpu_ctx
     bool land_spin = true;             // pbgpu_land_wait polls (PBGPU_LAND_SPIN=0: blocking waits)
     uint2 *d_jump = nullptr;
     uint2 *d_lcg48 = nullptr;
-    uint32_t *d_orbit = nullptr; // pb_vline_kernel: LCG-orbit prefix sums (built on first use, 8 MiB)
+    uint32_t *d_orbit = nullptr; // pb_vline_kernel: LCG-orbit prefix sums (built on first use, 2 MiB)
     uint32_t orbit_tot = 0;
     unsigned long long *d_dbg = nullptr; // PBGPU_TIMING: per-workgroup phase stamps
     uint64_t dbg_cap = 0;

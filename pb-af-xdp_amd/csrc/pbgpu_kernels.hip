@@ -309,6 +309,15 @@ __device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t
 // checksum position at compile time; RANDOM selects the payload source.  The
 // frame body is straight-line code (no data-dependent control flow on d[]).
 
+// (A/B builds only) the frame length as a compile-time constant in pb_small_kernel: what the
+// runtime length's uniform branches and masks cost
+#ifndef PB_SMALL_CFLEN
+#define PB_SMALL_CFLEN 0
+#endif
+#ifndef PB_SMALL_FMASK
+#define PB_SMALL_FMASK 1
+#endif
+
 // keep bytes [lo, hi) of a dword (byte positions 0..3), branch-free
 __device__ __forceinline__ uint32_t pb_range_mask(int lo, int hi)
 {
@@ -328,7 +337,7 @@ __device__ __forceinline__ void pb_small_frame(const pb_kargs &K, uint64_t fidx,
     constexpr int P0 = (HL - 2) / 4;                                 // payload byte 0 = byte 2 of dword P0
     constexpr int CDW = PROTO == 17 ? 10 : (PROTO == 6 ? 12 : 9);   // L4 checksum dword
     constexpr int CSH = PROTO == 6 ? 16 : 0;                         // ... and its half
-    const uint32_t flen = K.fixed_len;
+    const uint32_t flen = PB_SMALL_CFLEN ? PB_SMALL_CFLEN : K.fixed_len;
     const uint32_t flags = K.flags;
     const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + fidx);
     const uint32_t r0 = pb_rand_r(s);
@@ -362,10 +371,12 @@ __device__ __forceinline__ void pb_small_frame(const pb_kargs &K, uint64_t fidx,
         for (int t = P0; t < NDW; ++t)
             d[t] |= K.stail[t - P0];
     }
+#if PB_SMALL_FMASK
     // bytes past the frame end
 #pragma unroll
     for (int t = 0; t < NDW; ++t)
         d[t] &= pb_range_mask(0, (int)flen - 4 * t);
+#endif
 
     // L4 checksum (csum_tcpudp_magic / icmp_csum, sequence.c:569-594)
     uint32_t sum = d[8] >> 16;
@@ -486,7 +497,7 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
     const uint64_t f0 = (uint64_t)(PB_SMALL_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x) : blockIdx.x) * WGT;
     const uint64_t left = K.n_frames - f0;
     const uint32_t nfr = left < WGT ? (uint32_t)left : WGT;
-    const uint32_t flen = K.fixed_len;
+    const uint32_t flen = PB_SMALL_CFLEN ? PB_SMALL_CFLEN : K.fixed_len;
 
     if (tid < nfr)
     {
@@ -2146,6 +2157,9 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     return pb_fold(s);
 }
 
+#ifndef PB_VL_SPLIT
+#define PB_VL_SPLIT 1
+#endif
 template <int HL, bool L4>
 __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
 {
@@ -2344,34 +2358,49 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     const uint32_t nsteps = (R + PB_VL_STEP - 1u) / PB_VL_STEP;
     const uint32_t k = lane & 7u, kk = k | (k << 4), ck = (lo_rel >> 4) + k;
     const uint32_t lmax = nlines ? nlines - 1u : 0u;
-    for (uint32_t s = 0; s < nsteps; ++s)
+    // chunk i of step s; clamp: lines past the region's end are computed on its last line
+    auto chunk = [&](uint32_t s, uint32_t i, bool clamp) -> pb_u32x4 {
+        uint32_t l = s * (PB_VL_STEP / 128u) + (wv << 5) + (i << 3) + (lane >> 3);
+        if (clamp)
+            l = min(l, lmax);
+        const uint32_t ci = (l << 3) + ck;
+        const uint32_t t = (uint32_t)s_map[l] + kk;
+        const uint32_t f = (t >> 8) + __popc(t & 0x88u);
+        const pb_u32x4 rc = s_rec[f];
+        const uint32_t m = ci - rc[0]; // chunk index within frame f
+        const uint2 L = s_l48[m];
+        const uint32_t x = __umul24(rc[3], L.x) + L.y;
+        const int32_t pb = (int32_t)(ci << 4);
+        const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
+        const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
+        const pb_u32x4 h = s_img[f * NSP + min(m, NSP)];
+        const pb_u32x4 ml = s_m16[plo], mh = s_m16[phi];
+        uint32_t o0, o1, o2, o3;
+        pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+        const uint32_t M0 = ml[0] & ~mh[0], M1 = ml[1] & ~mh[1], M2 = ml[2] & ~mh[2], M3 = ml[3] & ~mh[3];
+        return pb_u32x4{(o0 & M0) | (h[0] & ~M0), (o1 & M1) | (h[1] & ~M1), (o2 & M2) | (h[2] & ~M2),
+                        (o3 & M3) | (h[3] & ~M3)};
+    };
+    // steps that lie wholly inside the region: no clamp, no store guard (their four chunks' LCG
+    // chains interleave instead of each running inside its own store branch)
+    const uint32_t nfull = (store && PB_VL_SPLIT) ? R / PB_VL_STEP : 0u;
+    for (uint32_t s = 0; s < nfull; ++s)
     {
-        // four independent chunks per lane, computed before any is stored (straight-line: their
-        // LDS reads and LCG chains overlap); lines past the region's end are computed on its last
-        // line and not stored
         pb_u32x4 v[4];
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
-        {
-            const uint32_t l = min(s * (PB_VL_STEP / 128u) + (wv << 5) + (i << 3) + (lane >> 3), lmax);
-            const uint32_t ci = (l << 3) + ck;
-            const uint32_t t = (uint32_t)s_map[l] + kk;
-            const uint32_t f = (t >> 8) + __popc(t & 0x88u);
-            const pb_u32x4 rc = s_rec[f];
-            const uint32_t m = ci - rc[0]; // chunk index within frame f
-            const uint2 L = s_l48[m];
-            const uint32_t x = __umul24(rc[3], L.x) + L.y;
-            const int32_t pb = (int32_t)(ci << 4);
-            const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
-            const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
-            const pb_u32x4 h = s_img[f * NSP + min(m, NSP)];
-            const pb_u32x4 ml = s_m16[plo], mh = s_m16[phi];
-            uint32_t o0, o1, o2, o3;
-            pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
-            const uint32_t M0 = ml[0] & ~mh[0], M1 = ml[1] & ~mh[1], M2 = ml[2] & ~mh[2], M3 = ml[3] & ~mh[3];
-            v[i] = pb_u32x4{(o0 & M0) | (h[0] & ~M0), (o1 & M1) | (h[1] & ~M1), (o2 & M2) | (h[2] & ~M2),
-                            (o3 & M3) | (h[3] & ~M3)};
-        }
+            v[i] = chunk(s, i, false);
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            pb_st16(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
+    }
+    for (uint32_t s = nfull; s < nsteps; ++s)
+    {
+        // four independent chunks per lane, computed before any is stored
+        pb_u32x4 v[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            v[i] = chunk(s, i, true);
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
         {

@@ -59,7 +59,7 @@ def test_bench_json_line():
     assert d["udp_1500"]["kernel"].startswith("pb_fstage_kernel")
     # the write-roofline probe: every shape reported, the fastest named
     shapes = d["write_peak_probe_shapes_gbps"]
-    assert len(shapes) == 12 and d["write_peak_probe_shape"] in shapes
+    assert len(shapes) == 15 and d["write_peak_probe_shape"] in shapes
     assert d["write_peak_probe_gbps"] == max(shapes.values())
 
 
