@@ -177,9 +177,16 @@ struct pb_kargs
 // record and nsp 16-B header chunks, a zero chunk and 17 chunk masks, the lcg48 entries, the
 // line map (u16)
 #define PB_VL_STEP 16384u // bytes of a workgroup's region per step (4 waves x 4 KiB)
-#define PB_ORB_SH 5       // orbit prefix sums sampled every 2^PB_ORB_SH positions (2 MiB table)
-#define PB_VL_LDS(wgf, nsp, nl48, nlines)                                                                     \
-    ((size_t)256 + ((size_t)(wgf) + PB_VST_GHOSTS) * 16 * (1 + (size_t)(nsp)) + 18 * 16 + (size_t)(nl48) * 8 + \
+#ifndef PB_ORB_SH
+#define PB_ORB_SH 5 // orbit prefix sums sampled every 2^PB_ORB_SH positions (2 MiB table)
+#endif
+#ifndef PB_VL_MT
+#define PB_VL_MT 1 // pb_vline_kernel's chunk masks: one table row per (plo + phi) (0: two rows, ANDed)
+#endif
+#define PB_VL_NMASK (PB_VL_MT ? 33 : 17)
+#define PB_VL_LDS(wgf, nsp, nl48, nlines)                                                                       \
+    ((size_t)256 + ((size_t)(wgf) + PB_VST_GHOSTS) * 16 * (1 + (size_t)(nsp)) + (1 + PB_VL_NMASK) * 16 +         \
+     (size_t)(nl48) * 8 +                                                                                        \
      (((size_t)(nlines) + 7) & ~(size_t)7) * 2)
 #define PB_VST_LDS(wgf) ((size_t)PB_STAGE_L48 * 8 + PB_VST_PRO + PB_VST_CAP(wgf) * (PB_VST_HVN + 5) * 4 + (PB_VST_CAP(wgf) + 2) * 4)
 

@@ -309,13 +309,8 @@ __device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t
 // checksum position at compile time; RANDOM selects the payload source.  The
 // frame body is straight-line code (no data-dependent control flow on d[]).
 
-// (A/B builds only) the frame length as a compile-time constant in pb_small_kernel: what the
-// runtime length's uniform branches and masks cost
-#ifndef PB_SMALL_CFLEN
-#define PB_SMALL_CFLEN 0
-#endif
-#ifndef PB_SMALL_FMASK
-#define PB_SMALL_FMASK 1
+#ifndef PB_RANGE_LDS
+#define PB_RANGE_LDS 0 // (A/B builds) pb_xpage_kernel reads the CIDR table from LDS
 #endif
 
 // keep bytes [lo, hi) of a dword (byte positions 0..3), branch-free
@@ -330,20 +325,24 @@ __device__ __forceinline__ uint32_t pb_range_mask(int lo, int hi)
 
 // One whole frame of <= 4*NDW bytes in VGPRs (iteration k = first_iter + fidx,
 // sequence.c:433-602): header fields, payload, L4 and IPv4 checksums.
+// rtab: (A/B builds, PB_RANGE_LDS) the CIDR table staged in LDS; null: K.ranges (global / L1)
 template <int NDW, int PROTO, bool RANDOM>
-__device__ __forceinline__ void pb_small_frame(const pb_kargs &K, uint64_t fidx, uint32_t (&d)[NDW])
+__device__ __forceinline__ void pb_small_frame(const pb_kargs &K, uint64_t fidx, uint32_t (&d)[NDW],
+                                               const uint2 *rtab = nullptr)
 {
     constexpr int HL = PROTO == 6 ? 54 : 42;
     constexpr int P0 = (HL - 2) / 4;                                 // payload byte 0 = byte 2 of dword P0
     constexpr int CDW = PROTO == 17 ? 10 : (PROTO == 6 ? 12 : 9);   // L4 checksum dword
     constexpr int CSH = PROTO == 6 ? 16 : 0;                         // ... and its half
-    const uint32_t flen = PB_SMALL_CFLEN ? PB_SMALL_CFLEN : K.fixed_len;
+    const uint32_t flen = K.fixed_len;
     const uint32_t flags = K.flags;
     const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + fidx);
     const uint32_t r0 = pb_rand_r(s);
     const uint32_t plen = flen - HL;
     uint32_t h[16];
-    const uint32_t l4tot = pb_header(K, r0, plen, h, pb_range(K, r0));
+    const uint32_t l4tot =
+        pb_header(K, r0, plen, h,
+                  (rtab && (flags & PBK_RND_SADDR) && K.rng.d != 1) ? rtab[pb_mod(r0, K.rng)] : pb_range(K, r0));
 #pragma unroll
     for (int t = 0; t < NDW; ++t)
         d[t] = t < 16 ? h[t] : 0u;
@@ -371,18 +370,27 @@ __device__ __forceinline__ void pb_small_frame(const pb_kargs &K, uint64_t fidx,
         for (int t = P0; t < NDW; ++t)
             d[t] |= K.stail[t - P0];
     }
-#if PB_SMALL_FMASK
-    // bytes past the frame end
-#pragma unroll
-    for (int t = 0; t < NDW; ++t)
-        d[t] &= pb_range_mask(0, (int)flen - 4 * t);
-#endif
+    // (no bytes past the frame end to clear: the template is zero past the header, the random
+    // payload is masked to its length above and the static one is zero past its bytes; clearing
+    // them again cost the 106-B UDP frame 8%, profiles/r03/ab/small_*)
 
     // L4 checksum (csum_tcpudp_magic / icmp_csum, sequence.c:569-594)
     uint32_t sum = d[8] >> 16;
+    if (RANDOM)
+    {
 #pragma unroll
-    for (int t = 9; t < NDW; ++t)
-        sum = pb_add_halves(sum, d[t]);
+        for (int t = 9; t < NDW; ++t)
+            sum = pb_add_halves(sum, d[t]);
+    }
+    else
+    {
+        // static payload: the header words, then the payload's precomputed word sum (it starts at
+        // byte 2 of dword P0, an even L4 offset)
+#pragma unroll
+        for (int t = 9; t < P0; ++t)
+            sum = pb_add_halves(sum, d[t]);
+        sum += (d[P0] & 0xFFFFu) + K.pl0.ssum;
+    }
     if (PROTO != 1)
         sum += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((PROTO + l4tot) << 8);
     const uint32_t c = (flags & PBK_L4_CSUM) ? ((~pb_fold(sum)) & 0xFFFFu) : 0u;
@@ -437,20 +445,21 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
         // half dword at one end and nw = (flen - 2) / 4 whole dwords, written two per
         // ds_write2_b32 (4-B alignment is all a pair needs) instead of dword + byte writes
         const uint32_t nw = (flen - 2u) >> 2;
-        const bool odd = (B & 2u) != 0; // starts at byte 2 of a dword: the half dword comes first
-        uint16_t *const half = reinterpret_cast<uint16_t *>(s_tile) + ((odd ? B : B + flen - 2u) >> 1);
-        *half = (uint16_t)(odd ? d[0] : (d[nw] & 0xFFFFu));
-        uint32_t *const row = s_tile + ((B + (odd ? 2u : 0u)) >> 2);
+        const uint32_t sh = B & 2u; // 2: starts at byte 2 of a dword, the half dword comes first
+        uint16_t *const half = reinterpret_cast<uint16_t *>(s_tile) + ((sh ? B : B + flen - 2u) >> 1);
+        *half = (uint16_t)(sh ? d[0] : (d[nw] & 0xFFFFu));
+        uint32_t *const row = s_tile + ((B + sh) >> 2);
 #pragma unroll
         for (int u = 0; u < NDW; u += 2)
         {
             if ((uint32_t)u < nw)
             {
-                const uint32_t v0 = odd ? __builtin_amdgcn_alignbyte(d[u + 1], d[u], 2u) : d[u];
+                // v_alignbyte by sh bytes: the frame's dwords as they are (sh = 0) or moved down two
+                // bytes (no select per dword)
+                const uint32_t v0 = __builtin_amdgcn_alignbyte(d[u + 1], d[u], sh);
                 if ((uint32_t)u + 1u < nw)
                 {
-                    const uint32_t v1 =
-                        odd ? __builtin_amdgcn_alignbyte(u + 2 < NDW ? d[u + 2] : 0u, d[u + 1], 2u) : d[u + 1];
+                    const uint32_t v1 = __builtin_amdgcn_alignbyte(u + 2 < NDW ? d[u + 2] : 0u, d[u + 1], sh);
                     const uint2 pr = make_uint2(v0, v1);
                     __builtin_memcpy(row + u, &pr, 8);
                 }
@@ -497,7 +506,7 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
     const uint64_t f0 = (uint64_t)(PB_SMALL_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x) : blockIdx.x) * WGT;
     const uint64_t left = K.n_frames - f0;
     const uint32_t nfr = left < WGT ? (uint32_t)left : WGT;
-    const uint32_t flen = PB_SMALL_CFLEN ? PB_SMALL_CFLEN : K.fixed_len;
+    const uint32_t flen = K.fixed_len;
 
     if (tid < nfr)
     {
@@ -675,6 +684,16 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[]; // K.xs_np page regions
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
+#if PB_RANGE_LDS
+    // (A/B) the CIDR table in LDS: one more barrier before the build
+    __shared__ uint2 s_rng[64];
+    if (tid < K.rng.d && tid < 64u && (K.flags & PBK_RND_SADDR))
+        s_rng[tid] = K.ranges[tid];
+    __syncthreads();
+    const uint2 *const rtab = s_rng;
+#else
+    const uint2 *const rtab = nullptr;
+#endif
     const uint32_t flen = K.fixed_len;
     const uint32_t np = K.xs_np, fpp = K.xp_fpp;
     const uint64_t T = K.total_bytes;
@@ -708,7 +727,7 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
         if (f >= K.n_frames || f * flen >= p0 + PB_XPG)
             continue;
         uint32_t d[NDW];
-        pb_small_frame<NDW, PROTO, RANDOM>(K, f, d);
+        pb_small_frame<NDW, PROTO, RANDOM>(K, f, d, rtab);
         const int off = (int)((int64_t)(f * flen) - (int64_t)p0); // (-flen, 4096), dword aligned
         uint32_t *row = s_tile + (i * PB_XREG + 128 + off) / 4;
 #pragma unroll
@@ -2075,12 +2094,11 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
 //    region's 128-B lines to the frame holding each line's first byte;
 //  * stream: the workgroup's byte region [lo, hi) (128-B aligned: no line has two writers) in
 //    16-KiB steps, wave w writing bytes [4 KiB w, 4 KiB (w + 1)) of a step as four 1-KiB store
-//    instructions (lane l: chunk l of each KiB).  A chunk that lies inside one frame's payload
-//    ("pure") is generated from the frame's record (line map -> record -> L^(48 m) entry) and
-//    stored; the others — the few chunks that hold header bytes or a frame edge — are left out,
-//    and after each step's payload chunks a pair of waves writes the "special" chunks of the
-//    frames whose first chunk lies in the step: header chunk | the previous frame's payload tail
-//    | the frame's own first payload bytes, each from one generated chunk and a mask.
+//    instructions (lane l: chunk l of each KiB).  Every chunk takes one straight-line path: the
+//    line map gives the frame holding its first byte (and where the next frame starts in the
+//    line), the frame's record its chunk index m and payload byte range, the L^(48 m) entry its
+//    LCG state; 16 payload bytes are generated and blended under a byte mask with the frame's
+//    shifted header image (header chunks) or the next frame's first header chunk (a frame edge).
 // Every byte of [lo, hi) is stored exactly once, whole 16-B chunks only (the launch's last chunk
 // zero-padded past the last frame).  Requires payloads of >= 32 bytes (a chunk then holds bytes
 // of at most two frames, and never a payload end and the next header end).
@@ -2111,6 +2129,21 @@ constexpr uint32_t pb_orb_c(int i)
     return c;
 }
 
+// M^-1 mod 2^24: y -> a^-1 (y - c)
+constexpr uint32_t pb_inv24(uint32_t a)
+{
+    uint32_t x = a; // Newton: x = x (2 - a x), each step doubles the correct low bits (a odd)
+    for (int i = 0; i < 5; ++i)
+        x = x * (2u - a * x);
+    return x & PB_M24;
+}
+constexpr uint32_t PB_A3I = pb_inv24(PB_A3 & PB_M24);
+constexpr uint32_t PB_C3I = (0u - PB_A3I * (PB_C3 & PB_M24)) & PB_M24;
+static_assert(((PB_A3I * (PB_A3 & PB_M24)) & PB_M24) == 1u, "M^-1");
+#ifndef PB_ORB_BIDIR
+#define PB_ORB_BIDIR 1 // pb_orbit_sum walks to the nearer prefix-sum sample (<= 16 steps; 0: the next, <= 31)
+#endif
+
 // Little-endian 16-bit word sum (mod 0xFFFF, in [1, 0xFFFF]) of the n >= 3 payload bytes drawn
 // from the LCG state st0 entering the payload (sequence.c:552-555), payload at an even L4 offset:
 // the value fold(sum of the bytes' words) takes (the orbit has no run of 3 zero bytes, so the true
@@ -2133,6 +2166,38 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     uint32_t q = p + n, wrap = 0;
     if (q >= (1u << 24)) // the run wraps the orbit (2^24 is even: parities keep)
         q -= 1u << 24, wrap = K.orbit_tot;
+#if PB_ORB_BIDIR
+    // prefix sums at p and q from the nearer sampled position (floor or ceil, <= 16 steps): walk the
+    // bytes in between with M (forward, subtract) or M^-1 (backward, add); a[t & 1] collects the
+    // walked bytes of one parity, the first walked position having parity par
+    constexpr uint32_t SM = (1u << PB_ORB_SH) - 1u, HALF = (SM + 1u) >> 1;
+    const bool fp = (p & SM) > HALF, fq = (q & SM) > HALF; // forward to the next sample
+    const uint32_t tp = K.orbit[(p >> PB_ORB_SH) + (fp ? 1u : 0u)], tq = K.orbit[(q >> PB_ORB_SH) + (fq ? 1u : 0u)];
+    const uint32_t dp = fp ? SM + 1u - (p & SM) : (p & SM), dq = fq ? SM + 1u - (q & SM) : (q & SM);
+    const uint32_t ap_ = fp ? PB_A3 & PB_M24 : PB_A3I, cp_ = fp ? PB_C3 & PB_M24 : PB_C3I;
+    const uint32_t aq_ = fq ? PB_A3 & PB_M24 : PB_A3I, cq_ = fq ? PB_C3 & PB_M24 : PB_C3I;
+    uint32_t y = fp ? yp : __umul24(yp, PB_A3I) + PB_C3I; // backward: from position p - 1
+    uint32_t z = fq ? yq : __umul24(yq, PB_A3I) + PB_C3I;
+    uint32_t ap[2] = {0u, 0u}, aq[2] = {0u, 0u};
+#pragma unroll
+    for (uint32_t t = 0; t < HALF; ++t)
+    {
+        ap[t & 1u] += t < dp ? (y >> 16) & 0xFFu : 0u;
+        aq[t & 1u] += t < dq ? (z >> 16) & 0xFFu : 0u;
+        y = __umul24(y, ap_) + cp_;
+        z = __umul24(z, aq_) + cq_;
+    }
+    // even / odd position sums of the walked bytes (the first walked position: p, or p - 1)
+    const uint32_t pp = fp ? p & 1u : (p & 1u) ^ 1u, pq = fq ? q & 1u : (q & 1u) ^ 1u;
+    const uint32_t sEp = ap[pp], sOp = ap[pp ^ 1u], sEq = aq[pq], sOq = aq[pq ^ 1u];
+    // PE / PO at p and q, each in [0, 2 * 0xFFFF)
+    const uint32_t PEp = fp ? (tp & 0xFFFFu) + 0xFFFFu - sEp : (tp & 0xFFFFu) + sEp;
+    const uint32_t POp = fp ? (tp >> 16) + 0xFFFFu - sOp : (tp >> 16) + sOp;
+    const uint32_t PEq = fq ? (tq & 0xFFFFu) + 0xFFFFu - sEq : (tq & 0xFFFFu) + sEq;
+    const uint32_t POq = fq ? (tq >> 16) + 0xFFFFu - sOq : (tq >> 16) + sOq;
+    const uint32_t de = PEq + wrap + 2u * 0xFFFFu - PEp;
+    const uint32_t dO = POq + wrap + 2u * 0xFFFFu - POp;
+#else
     constexpr uint32_t SM = (1u << PB_ORB_SH) - 1u;
     const uint32_t tp = K.orbit[(p + SM) >> PB_ORB_SH], tq = K.orbit[(q + SM) >> PB_ORB_SH];
     // prefix sums at p and q from the next sampled position, minus the bytes in between (walked
@@ -2152,6 +2217,7 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     // PE(q) - PE(p), PO(q) - PO(p), kept positive with multiples of 0xFFFF
     const uint32_t de = (tq & 0xFFFFu) + wrap + e_p + 2u * 0xFFFFu - e_q - (tp & 0xFFFFu);
     const uint32_t dO = (tq >> 16) + wrap + o_p + 2u * 0xFFFFu - o_q - (tp >> 16);
+#endif
     // payload byte j sits at orbit position p + j: even j is a word's low byte
     const uint32_t s = (p & 1u) ? dO + (de << 8) : de + (dO << 8);
     return pb_fold(s);
@@ -2159,6 +2225,9 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
 
 #ifndef PB_VL_SPLIT
 #define PB_VL_SPLIT 1
+#endif
+#ifndef PB_VL_IMGW
+#define PB_VL_IMGW 1 // prologue: header images as NHW dword writes, line map as plain writes + the last line
 #endif
 template <int HL, bool L4>
 __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
@@ -2174,7 +2243,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     pb_u32x4 *const s_rec = reinterpret_cast<pb_u32x4 *>(s_dyn + 64); // {start, end, z, -} per frame slot
     pb_u32x4 *const s_img = s_rec + CAP;                              // NSP header chunks per frame slot
     pb_u32x4 *const s_m16 = s_img + CAP * NSP + 1;                    // after one zero chunk: byte masks
-    uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_m16 + 17);
+    uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_m16 + PB_VL_NMASK);
     uint16_t *const s_map = reinterpret_cast<uint16_t *>(s_l48 + K.vl_nl48);
 
     const uint32_t tid = threadIdx.x;
@@ -2297,6 +2366,17 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             const uint32_t lo = u > 0 ? d[u - 1] : 0u, hi = u < 16 ? d[u] : 0u;
             v[u] = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
         }
+#if PB_VL_IMGW
+        // only the header bytes [s0, s0 + HL) of the image chunks are ever read (bytes before s0
+        // belong to the previous frame's chunk and take its payload, bytes after the header this
+        // frame's payload): NHW dwords from dword q, inside the frame's own NSP chunks
+        constexpr uint32_t NHW = (HL + 6) / 4;
+        static_assert(3 + NHW <= 4 * NSP, "image slot");
+        uint32_t *const img32 = reinterpret_cast<uint32_t *>(s_img + (uint32_t)tix * NSP) + q;
+#pragma unroll
+        for (uint32_t u = 0; u < NHW; ++u)
+            img32[u] = v[u];
+#else
         pb_u32x4 *const img = s_img + (uint32_t)tix * NSP;
 #pragma unroll
         for (uint32_t j = 0; j < NSP; ++j)
@@ -2314,6 +2394,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             }
             img[j] = pb_u32x4{o[0], o[1], o[2], o[3]};
         }
+#endif
     }
     __syncthreads();
 
@@ -2332,17 +2413,38 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         // 8: none), kept as 8 - c in bits 0-2 and 4-6: chunk k of the line lies in frame
         // tix + (k >= c1) + (k >= c2), and k >= c <=> k + (8 - c) carries into bit 3 / 7
         const uint32_t b2 = (uint32_t)tix + 1u < nfr ? s_rec[tix + 1][2] - lo_rel : 0xFFFFFFFFu;
+#if PB_VL_IMGW
+        // only the frame's last line can hold the next frame starts (o1, o2 >= 128 before it)
+        for (uint32_t L = la; L + 1u < lb; ++L)
+            s_map[L] = (uint16_t)((uint32_t)tix << 8);
+        if (la < lb)
+        {
+            const uint32_t L = lb - 1u;
+#else
         for (uint32_t L = la; L < lb; ++L)
         {
+#endif
             const uint32_t o1 = b - (L << 7), o2 = b2 - (L << 7);
             const uint32_t c1 = o1 < 128u ? (o1 + 15u) >> 4 : 8u, c2 = o2 < 128u ? (o2 + 15u) >> 4 : 8u;
             s_map[L] = (uint16_t)(((uint32_t)tix << 8) | (8u - c1) | ((8u - c2) << 4));
         }
     }
+#if PB_VL_MT
+    // chunk byte masks, indexed by plo + phi: a chunk holds a payload start (plo > 0, phi = 16) or
+    // a payload end (plo = 0, phi < 16) or neither (payloads of >= 32 B), so s_m16[j] keeps bytes
+    // < j for j <= 16 and bytes >= j - 16 above
+    if (tid <= 32u)
+    {
+        const int lo = tid > 16u ? (int)tid - 16 : 0, hi = tid > 16u ? 16 : (int)tid;
+        s_m16[tid] = pb_u32x4{pb_range_mask(lo, hi), pb_range_mask(lo - 4, hi - 4), pb_range_mask(lo - 8, hi - 8),
+                              pb_range_mask(lo - 12, hi - 12)};
+    }
+#else
     if (tid <= 16u) // chunk byte masks: s_m16[k] keeps bytes >= k
         s_m16[tid] = pb_u32x4{pb_range_mask((int)tid, 4), pb_range_mask((int)tid - 4, 4), pb_range_mask((int)tid - 8, 4),
                               pb_range_mask((int)tid - 12, 4)};
-    if (tid == 32u) // the header chunk after the last record's: no frame starts there
+#endif
+    if (tid == 64u) // the header chunk after the last record's: no frame starts there
         s_img[nfr * NSP] = pb_u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
 
@@ -2355,7 +2457,8 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     // One straight-line path per chunk, and every 128-B line leaves in one store instruction.
     uint8_t *const gout = K.out + wbase + lo_rel;
     const bool store = !(K.fst_dbg & 2u);
-    const uint32_t nsteps = (R + PB_VL_STEP - 1u) / PB_VL_STEP;
+    // (PBGPU_FST_DBG bit 0, diagnostics: the prologue alone, no stream)
+    const uint32_t nsteps = (K.fst_dbg & 1u) ? 0u : (R + PB_VL_STEP - 1u) / PB_VL_STEP;
     const uint32_t k = lane & 7u, kk = k | (k << 4), ck = (lo_rel >> 4) + k;
     const uint32_t lmax = nlines ? nlines - 1u : 0u;
     // chunk i of step s; clamp: lines past the region's end are computed on its last line
@@ -2374,16 +2477,21 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
         const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
         const pb_u32x4 h = s_img[f * NSP + min(m, NSP)];
-        const pb_u32x4 ml = s_m16[plo], mh = s_m16[phi];
         uint32_t o0, o1, o2, o3;
         pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+#if PB_VL_MT
+        const pb_u32x4 mm = s_m16[plo + phi]; // payload bytes [plo, phi)
+        const uint32_t M0 = mm[0], M1 = mm[1], M2 = mm[2], M3 = mm[3];
+#else
+        const pb_u32x4 ml = s_m16[plo], mh = s_m16[phi];
         const uint32_t M0 = ml[0] & ~mh[0], M1 = ml[1] & ~mh[1], M2 = ml[2] & ~mh[2], M3 = ml[3] & ~mh[3];
+#endif
         return pb_u32x4{(o0 & M0) | (h[0] & ~M0), (o1 & M1) | (h[1] & ~M1), (o2 & M2) | (h[2] & ~M2),
                         (o3 & M3) | (h[3] & ~M3)};
     };
     // steps that lie wholly inside the region: no clamp, no store guard (their four chunks' LCG
     // chains interleave instead of each running inside its own store branch)
-    const uint32_t nfull = (store && PB_VL_SPLIT) ? R / PB_VL_STEP : 0u;
+    const uint32_t nfull = (store && PB_VL_SPLIT) ? min(nsteps, R / PB_VL_STEP) : 0u;
     for (uint32_t s = 0; s < nfull; ++s)
     {
         pb_u32x4 v[4];
