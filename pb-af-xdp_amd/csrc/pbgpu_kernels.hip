@@ -309,6 +309,9 @@ __device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t
 // checksum position at compile time; RANDOM selects the payload source.  The
 // frame body is straight-line code (no data-dependent control flow on d[]).
 
+#ifndef PB_SMALL_RBATCH
+#define PB_SMALL_RBATCH 1 // pb_small_kernel: all of a lane's tile reads before its stores
+#endif
 #ifndef PB_RANGE_LDS
 #define PB_RANGE_LDS 0 // (A/B builds) pb_xpage_kernel reads the CIDR table from LDS
 #endif
@@ -521,6 +524,33 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
     const uint32_t nchunks = (tile_bytes + 15) >> 4;
     uint8_t *const out = K.out + f0 * flen;
     const bool swz = (flen & 7u) == 0;
+#if PB_SMALL_RBATCH
+    // every LDS read of the lane first, then the stores (the reads' latencies overlap instead of
+    // one read -> wait -> store round trip per chunk)
+    constexpr uint32_t NCK = NDW / 4; // the most chunks per lane: WGT * 4 NDW bytes / 16 / WGT
+    pb_u32x4 v[NCK];
+#pragma unroll
+    for (uint32_t k = 0; k < NCK; ++k)
+    {
+        const uint32_t c = tid + k * WGT;
+        v[k] = reinterpret_cast<const pb_u32x4 *>(s_tile)[min(swz ? pb_swz(c) : c, (uint32_t)(WGT * NDW / 4 - 1))];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < NCK; ++k)
+    {
+        const uint32_t c = tid + k * WGT;
+        if (c < nchunks)
+        {
+            if (16 * c + 16 > tile_bytes) // last chunk of the stream: zero the tail
+            {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    v[k][t] &= pb_range_mask(0, (int)tile_bytes - (int)(16 * c + 4 * t));
+            }
+            pb_st16(out + 16 * c, v[k]);
+        }
+    }
+#else
     for (uint32_t c = tid; c < nchunks; c += WGT)
     {
         pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[swz ? pb_swz(c) : c];
@@ -532,6 +562,7 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
         }
         pb_st16(out + 16 * c, v);
     }
+#endif
     if (tid == 0)
         pb_count(K, blockIdx.x, nfr, tile_bytes);
 }
@@ -2226,6 +2257,9 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
 #ifndef PB_VL_SPLIT
 #define PB_VL_SPLIT 1
 #endif
+#ifndef PB_VL_SYNC
+#define PB_VL_SYNC 0
+#endif
 #ifndef PB_VL_IMGW
 #define PB_VL_IMGW 1 // prologue: header images as NHW dword writes, line map as plain writes + the last line
 #endif
@@ -2501,6 +2535,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
             pb_st16(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
+#if PB_VL_SYNC
+        __syncthreads(); // (A/B) the four waves' stores stay in one 16-KiB step
+#endif
     }
     for (uint32_t s = nfull; s < nsteps; ++s)
     {

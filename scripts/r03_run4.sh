@@ -12,8 +12,9 @@ echo "rc=$rc" >> $O/pytest.log
 [ $rc -ne 0 ] && exit $rc
 L=pb-af-xdp_amd/lib/libpbgpu.so
 V=pb-af-xdp_amd/lib/variants
-REPS=6 timeout -k 10 300 python -u scripts/ab_lib.py c3_udp_var 33554432 cur:$L base:$V/libpbgpu_base.so \
-    nomt:$V/libpbgpu_nomt.so nobidir:$V/libpbgpu_nobidir.so noimgw:$V/libpbgpu_noimgw.so > $O/ab_c3.jsonl 2>&1 || exit 1
+REPS=5 timeout -k 10 400 python -u scripts/ab_lib.py c3_udp_var 33554432 cur:$L base:$V/libpbgpu_base.so \
+    nomt:$V/libpbgpu_nomt.so nobidir:$V/libpbgpu_nobidir.so noimgw:$V/libpbgpu_noimgw.so orb4:$V/libpbgpu_orb4.so \
+    orb6:$V/libpbgpu_orb6.so > $O/ab_c3.jsonl 2>&1 || exit 1
 REPS=8 timeout -k 10 200 python -u scripts/ab_lib.py c5_icmp_echo 33554432 cur:$L base:$V/libpbgpu_base.so \
     > $O/ab_icmp98.jsonl 2>&1 || exit 1
 REPS=8 timeout -k 10 200 python -u scripts/ab_lib.py c1_udp_static_106 33554432 cur:$L base:$V/libpbgpu_base.so \
@@ -28,3 +29,7 @@ for cfg in c3_udp_var c5_icmp_echo; do
   done
 done
 echo PMC_DONE
+for v in orb4 orb6; do
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_c3_udp_var_${v}_FETCH_SIZE -o run -- \
+      python3 scripts/ab_lib.py c3_udp_var 33554432 $v:$V/libpbgpu_$v.so > $O/pmc_${v}.log 2>&1 || { echo "PMC_FAIL $v"; exit 1; }
+done
