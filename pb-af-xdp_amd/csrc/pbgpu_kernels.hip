@@ -309,9 +309,6 @@ __device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t
 // checksum position at compile time; RANDOM selects the payload source.  The
 // frame body is straight-line code (no data-dependent control flow on d[]).
 
-#ifndef PB_SMALL_RBATCH
-#define PB_SMALL_RBATCH 1 // pb_small_kernel: all of a lane's tile reads before its stores
-#endif
 #ifndef PB_RANGE_LDS
 #define PB_RANGE_LDS 0 // (A/B builds) pb_xpage_kernel reads the CIDR table from LDS
 #endif
@@ -524,33 +521,6 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
     const uint32_t nchunks = (tile_bytes + 15) >> 4;
     uint8_t *const out = K.out + f0 * flen;
     const bool swz = (flen & 7u) == 0;
-#if PB_SMALL_RBATCH
-    // every LDS read of the lane first, then the stores (the reads' latencies overlap instead of
-    // one read -> wait -> store round trip per chunk)
-    constexpr uint32_t NCK = NDW / 4; // the most chunks per lane: WGT * 4 NDW bytes / 16 / WGT
-    pb_u32x4 v[NCK];
-#pragma unroll
-    for (uint32_t k = 0; k < NCK; ++k)
-    {
-        const uint32_t c = tid + k * WGT;
-        v[k] = reinterpret_cast<const pb_u32x4 *>(s_tile)[min(swz ? pb_swz(c) : c, (uint32_t)(WGT * NDW / 4 - 1))];
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < NCK; ++k)
-    {
-        const uint32_t c = tid + k * WGT;
-        if (c < nchunks)
-        {
-            if (16 * c + 16 > tile_bytes) // last chunk of the stream: zero the tail
-            {
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    v[k][t] &= pb_range_mask(0, (int)tile_bytes - (int)(16 * c + 4 * t));
-            }
-            pb_st16(out + 16 * c, v[k]);
-        }
-    }
-#else
     for (uint32_t c = tid; c < nchunks; c += WGT)
     {
         pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[swz ? pb_swz(c) : c];
@@ -562,7 +532,6 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
         }
         pb_st16(out + 16 * c, v);
     }
-#endif
     if (tid == 0)
         pb_count(K, blockIdx.x, nfr, tile_bytes);
 }

@@ -27,8 +27,8 @@
 #include <unistd.h>
 
 #define PB_MAX_WORKERS 1024
-#define PB_LAND_INFLIGHT_MAX 16 /* landings queued per thread (PB_LAND_INFLIGHT, default 3) */
-#define PB_LAND_CHUNK_DEF 1024   /* frames per landing (PB_LAND_CHUNK; a quarter of the UMEM) */
+#define PB_LAND_INFLIGHT_MAX 16 /* landings queued per thread (PB_LAND_INFLIGHT, default 2) */
+#define PB_LAND_CHUNK_DEF 2048   /* frames per landing (PB_LAND_CHUNK; half of the UMEM) */
 
 static uint32_t env_u32(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi)
 {
@@ -450,7 +450,9 @@ static void *gpu_worker(void *p)
     /* landing granularity: frames per landing and landings in flight (their launch and
      * completion latencies overlap); tunable for the host-rate probe (scripts/e2e_probe.py) */
     const uint32_t land_chunk = env_u32("PB_LAND_CHUNK", PB_LAND_CHUNK_DEF, 1, nslots);
-    const uint32_t land_inflight = env_u32("PB_LAND_INFLIGHT", 3, 1, PB_LAND_INFLIGHT_MAX);
+    /* 64-B UDP, one TX thread (profiles/r03/e2e): 2048 x 2 129-137 Mpps, 1024 x 3 73, 512 x 6 34-43,
+     * 256 x 12 20-28 — each landing is a kernel launch and a host wait, so few large ones win */
+    const uint32_t land_inflight = env_u32("PB_LAND_INFLIGHT", 2, 1, PB_LAND_INFLIGHT_MAX);
     const double t0 = now_s();
     uint64_t my_frames = 0; /* this thread's frames: the delay pacing (per thread) */
     uint64_t step = 0;
