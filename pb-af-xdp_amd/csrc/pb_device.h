@@ -148,7 +148,6 @@ struct pb_kargs
     uint32_t vl_wgf;        // its own frames per workgroup (<= 256 - PB_VST_GHOSTS)
     uint32_t vl_nl48;       // lcg48 entries it keeps in LDS (chunks of the longest frame + 2)
     uint32_t vl_nlines;     // its line-map entries (128-B lines of the longest workgroup region)
-    uint32_t sw_nw;         // >0: small fixed frames through pb_swin_kernel, sw_nw windows of 256 frames per workgroup
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

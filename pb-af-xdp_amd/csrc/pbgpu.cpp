@@ -108,6 +108,8 @@ struct timing_pair
     hipEvent_t a, b;
 };
 
+#define PB_SEQ_STREAMS 4
+
 // What pbgpu_frames.reserved points to: the buffer's build-completion event (the landing
 // stream waits on it) and the completion event of the last landing queued from it (the
 // next build into the buffer waits on that, so a landing never reads frames being rebuilt)
@@ -116,6 +118,8 @@ struct frames_events
     hipEvent_t built = nullptr;
     hipEvent_t landed = nullptr;
     bool land_pending = false;
+    hipStream_t last = nullptr; // the stream the buffer was last built on
+    hipEvent_t moved = nullptr; // a build on another stream waits on this (recorded on `last`)
 };
 
 frames_events *frames_ev(pbgpu_frames *f)
@@ -147,6 +151,14 @@ struct pbgpu_ctx
     int timing_mode = PBGPU_TIMING_LAUNCH;
     timing_pair span = {nullptr, nullptr}; // PBGPU_TIMING_SPAN: first-launch / call events
     uint32_t span_n = 0;                    // launches in the open span (0: none open)
+    // PBGPU_TIMING_SPAN: the builds of sequence i run on seq_stream[i % PB_SEQ_STREAMS], so the
+    // kernels of different sequences overlap (as the reference's non-blocking sequences run
+    // their threads side by side, sequence.c:741-765); every other call first joins them
+    // into `stream` (one event per stream that built since the last join)
+    hipStream_t seq_stream[PB_SEQ_STREAMS] = {};
+    hipEvent_t seq_join[PB_SEQ_STREAMS] = {};
+    bool seq_dirty[PB_SEQ_STREAMS] = {};
+    bool seq_in_span[PB_SEQ_STREAMS] = {}; // has waited on span.a since it was recorded
     uint8_t *h_stage = nullptr;
     uint16_t *d_lens = nullptr; // landing: frame lengths of the mapped scatter (device), a ring
     uint16_t *h_lens = nullptr; // ... and their pinned host copy
@@ -419,6 +431,29 @@ int pbgpu_device_count(int *n)
     return PBGPU_OK;
 }
 
+// The sequence builds issued since the last join, ordered before what follows on ctx->stream.
+static int join_builds(pbgpu_ctx *ctx)
+{
+    for (int i = 0; i < PB_SEQ_STREAMS; ++i)
+        if (ctx->seq_dirty[i])
+        {
+            if (ctx->seq_join[i] == nullptr)
+                HIPCHK(hipEventCreateWithFlags(&ctx->seq_join[i], hipEventDisableTiming));
+            HIPCHK(hipEventRecord(ctx->seq_join[i], ctx->seq_stream[i]));
+            HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->seq_join[i], 0));
+            ctx->seq_dirty[i] = false;
+        }
+    return PBGPU_OK;
+}
+
+#define PB_JOIN(ctx)                         \
+    do                                       \
+    {                                        \
+        const int jrc_ = join_builds(ctx);   \
+        if (jrc_ != PBGPU_OK)                \
+            return jrc_;                     \
+    } while (0)
+
 int pbgpu_open(int device, pbgpu_ctx **out)
 {
     if (out == NULL)
@@ -470,6 +505,9 @@ void pbgpu_close(pbgpu_ctx *ctx)
     if (ctx == NULL)
         return;
     (void)hipSetDevice(ctx->device);
+    for (int i = 0; i < PB_SEQ_STREAMS; ++i)
+        if (ctx->seq_stream[i])
+            (void)hipStreamSynchronize(ctx->seq_stream[i]);
     if (ctx->stream)
         (void)hipStreamSynchronize(ctx->stream);
     if (ctx->land_stream)
@@ -507,6 +545,13 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipFree(ctx->d_lens);
     if (ctx->h_lens)
         (void)hipHostFree(ctx->h_lens);
+    for (int i = 0; i < PB_SEQ_STREAMS; ++i)
+    {
+        if (ctx->seq_join[i])
+            (void)hipEventDestroy(ctx->seq_join[i]);
+        if (ctx->seq_stream[i])
+            (void)hipStreamDestroy(ctx->seq_stream[i]);
+    }
     if (ctx->stream)
         (void)hipStreamDestroy(ctx->stream);
     if (ctx->land_stream)
@@ -521,6 +566,8 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     if (ctx == NULL || seq == NULL || seq_idx >= PB_MAX_SEQUENCES)
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
+    HIPCHK(hipStreamSynchronize(ctx->stream)); // no build still reads the slot's tables
     seq_slot &S = ctx->seqs[seq_idx];
     slot_free(S);
 
@@ -821,10 +868,6 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             if (enp > 0 && (uint32_t)enp * K.xp_fpp <= 2 * PB_WG)
                 K.xs_np = (uint32_t)enp;
         }
-        // windowed form (pb_swin_kernel) for the lengths the page kernels do not take: PBGPU_SMALL_WIN
-        // = windows of 256 frames per workgroup (0: the linear pb_small_kernel)
-        if (!K.xs_np || env_is("PBGPU_KERNEL", "linear"))
-            K.sw_nw = (uint32_t)std::min(64, std::max(0, env_int("PBGPU_SMALL_WIN", 0)));
         if (!pls[0].random)
         {
             const uint32_t p0 = (K.hl - 2) / 4;
@@ -1121,6 +1164,7 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
     {
         (void)hipSetDevice(ctx->device);
         (void)pbgpu_land_wait(ctx, 0);
+        (void)join_builds(ctx);
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamSynchronize(ctx->land_stream);
     }
@@ -1129,6 +1173,8 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
         frames_events *fe = (frames_events *)f->reserved;
         if (fe->built)
             (void)hipEventDestroy(fe->built);
+        if (fe->moved)
+            (void)hipEventDestroy(fe->moved);
         if (fe->landed)
             (void)hipEventDestroy(fe->landed);
         delete fe;
@@ -1190,7 +1236,7 @@ static void report_phase_timing(pbgpu_ctx *ctx, uint64_t n_wg)
 
 // The frames' build-completion event (kept in pbgpu_frames.reserved): the
 // landing stream waits on it, so landing one buffer overlaps building the next.
-static int mark_built(pbgpu_ctx *ctx, pbgpu_frames *out)
+static int mark_built(pbgpu_ctx *ctx, pbgpu_frames *out, hipStream_t st)
 {
     // only for callers that land frames: an event record per launch would cost a
     // release between back-to-back builds that are never landed (bench)
@@ -1201,7 +1247,7 @@ static int mark_built(pbgpu_ctx *ctx, pbgpu_frames *out)
         return PBGPU_ENOMEM;
     if (fe->built == nullptr)
         HIPCHK(hipEventCreateWithFlags(&fe->built, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(fe->built, ctx->stream));
+    HIPCHK(hipEventRecord(fe->built, st));
     return PBGPU_OK;
 }
 
@@ -1222,11 +1268,34 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     if (((max_bytes + 15) & ~15ull) > out->capacity_bytes)
         return PBGPU_ENOSPC;
 
-    // a landing queued from this buffer must have read it before the build overwrites it
-    if (out->reserved && ((frames_events *)out->reserved)->land_pending)
+    // the stream this build runs on: the sequence's own in span mode (builds of different
+    // sequences overlap), the context's otherwise (each launch timed on its own)
+    hipStream_t st = ctx->stream;
+    const bool span = ctx->timing_mode == PBGPU_TIMING_SPAN;
+    int si = -1;
+    if (span && !env_is("PBGPU_SEQ_STREAMS", "0"))
     {
-        frames_events *fe = (frames_events *)out->reserved;
-        HIPCHK(hipStreamWaitEvent(ctx->stream, fe->landed, 0));
+        si = seq_idx % PB_SEQ_STREAMS;
+        if (ctx->seq_stream[si] == nullptr)
+            HIPCHK(hipStreamCreateWithFlags(&ctx->seq_stream[si], hipStreamNonBlocking));
+        st = ctx->seq_stream[si];
+    }
+    frames_events *fe = frames_ev(out);
+    if (fe == NULL)
+        return PBGPU_ENOMEM;
+    // a buffer last built on another stream: this build follows that one
+    if (fe->last && fe->last != st)
+    {
+        if (fe->moved == nullptr)
+            HIPCHK(hipEventCreateWithFlags(&fe->moved, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(fe->moved, fe->last));
+        HIPCHK(hipStreamWaitEvent(st, fe->moved, 0));
+    }
+    fe->last = st;
+    // a landing queued from this buffer must have read it before the build overwrites it
+    if (fe->land_pending)
+    {
+        HIPCHK(hipStreamWaitEvent(st, fe->landed, 0));
         fe->land_pending = false;
     }
     pb_kargs K = S.K;
@@ -1264,8 +1333,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             uint32_t *bsum = reinterpret_cast<uint32_t *>(out->scan_tmp);
             unsigned long long *l2 =
                 reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(out->scan_tmp) + vst_bsum_bytes(nblk));
-            HIPCHK(pbk_launch_vst_lengths(&K, wgf, bsum, (uint32_t)nblk, l2, (uint32_t)n_l2, out->offsets,
-                                          ctx->stream));
+            HIPCHK(pbk_launch_vst_lengths(&K, wgf, bsum, (uint32_t)nblk, l2, (uint32_t)n_l2, out->offsets, st));
             K.vblk_sum = bsum;
             K.vblk_l2 = l2;
             K.offsets_w = out->offsets;
@@ -1273,8 +1341,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         else
         {
             const uint64_t nblocks = (nf + PB_SCAN_FRAMES_PER_BLOCK - 1) / PB_SCAN_FRAMES_PER_BLOCK;
-            HIPCHK(pbk_launch_lengths(&K, (unsigned long long *)out->scan_tmp, (uint32_t)nblocks, out->offsets,
-                                      ctx->stream));
+            HIPCHK(pbk_launch_lengths(&K, (unsigned long long *)out->scan_tmp, (uint32_t)nblocks, out->offsets, st));
         }
     }
     K.xs_grid = 0;
@@ -1290,7 +1357,6 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             K.xs_grid = K.xs_full + (uint32_t)((nch - (uint64_t)K.xs_full * np + np - 1) / np);
         }
     }
-    const bool span = ctx->timing_mode == PBGPU_TIMING_SPAN;
     timing_pair tp = {nullptr, nullptr};
     int rc = PBGPU_OK;
     if (!span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
@@ -1308,7 +1374,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             HIPCHK(hipMalloc((void **)&ctx->d_dbg, n_wg * 8 * sizeof(unsigned long long)));
             ctx->dbg_cap = n_wg;
         }
-        HIPCHK(hipMemsetAsync(ctx->d_dbg, 0, n_wg * 8 * sizeof(unsigned long long), ctx->stream));
+        HIPCHK(hipMemsetAsync(ctx->d_dbg, 0, n_wg * 8 * sizeof(unsigned long long), st));
         K.dbg = ctx->d_dbg;
     }
     if (span)
@@ -1321,15 +1387,26 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
                 HIPCHK(hipEventCreate(&ctx->span.b));
             }
             HIPCHK(hipEventRecord(ctx->span.a, ctx->stream));
+            for (bool &j : ctx->seq_in_span)
+                j = false;
         }
-        HIPCHK(pbk_launch_build(&K, ctx->stream));
+        if (si >= 0)
+        {
+            if (!ctx->seq_in_span[si]) // the span starts before this stream's first launch in it
+            {
+                HIPCHK(hipStreamWaitEvent(st, ctx->span.a, 0));
+                ctx->seq_in_span[si] = true;
+            }
+            ctx->seq_dirty[si] = true;
+        }
+        HIPCHK(pbk_launch_build(&K, st));
         ++ctx->span_n;
-        return mark_built(ctx, out);
+        return mark_built(ctx, out, st);
     }
     HIPCHK(hipEventRecord(tp.a, ctx->stream));
     HIPCHK(pbk_launch_build(&K, ctx->stream));
     HIPCHK(hipEventRecord(tp.b, ctx->stream));
-    if ((rc = mark_built(ctx, out)) != PBGPU_OK)
+    if ((rc = mark_built(ctx, out, st)) != PBGPU_OK)
         return rc;
     if (timing)
         report_phase_timing(ctx, n_wg);
@@ -1350,6 +1427,7 @@ int pbgpu_sync(pbgpu_ctx *ctx)
     if (ctx == NULL)
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PBGPU_OK;
 }
@@ -1365,6 +1443,7 @@ int pbgpu_frames_total(pbgpu_ctx *ctx, pbgpu_frames *f, uint64_t *total)
         return PBGPU_OK;
     }
     HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
     uint64_t t = 0;
     HIPCHK(hipMemcpyAsync(&t, f->offsets + f->n_frames, sizeof t, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1379,6 +1458,7 @@ int pbgpu_copy_packed(pbgpu_ctx *ctx, const pbgpu_frames *f, void *dst, uint64_t
     if (ctx == NULL || f == NULL || dst == NULL || byte_offset + nbytes > f->capacity_bytes)
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
     HIPCHK(hipMemcpyAsync(dst, f->data + byte_offset, nbytes, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PBGPU_OK;
@@ -1395,6 +1475,7 @@ int pbgpu_copy_offsets(pbgpu_ctx *ctx, const pbgpu_frames *f, uint64_t *dst)
             dst[i] = i * f->fixed_len;
         return PBGPU_OK;
     }
+    PB_JOIN(ctx);
     HIPCHK(hipMemcpyAsync(dst, f->offsets, (f->n_frames + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
                           ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1483,6 +1564,7 @@ int pbgpu_land_wait(pbgpu_ctx *ctx, uint32_t keep)
 static int land_unmapped(pbgpu_ctx *ctx, const pbgpu_frames *f, uint8_t *dst, uint32_t slot_stride,
                          uint64_t first_frame, uint32_t n, uint16_t *lens_out)
 {
+    PB_JOIN(ctx);
     int rc = pbgpu_land_wait(ctx, 0);
     if (rc != PBGPU_OK)
         return rc;
@@ -1546,6 +1628,7 @@ int pbgpu_copy_to_umem_async(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, 
                         ctx->seqs[f->seq_idx].max_flen > slot_stride))
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
     hipStream_t ls = ctx->land_stream;
     ctx->land_events = true;
     frames_events *fe = (frames_events *)f->reserved;
@@ -1637,6 +1720,7 @@ int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)
     if (ctx == NULL || n_seq < 0 || n_seq > PB_MAX_SEQUENCES)
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
     if (n_seq == 0)
         return PBGPU_OK;
     // the kernels' per-workgroup adds land in PB_CTR_SHARDS shards per sequence: sum them
@@ -1677,6 +1761,7 @@ int pbgpu_kernel_time(pbgpu_ctx *ctx, double *ms_total, uint32_t *n_launches)
     if (ctx == NULL)
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx); // the span ends after every sequence stream's launches
     double tot = 0;
     uint32_t n = 0;
     if (ctx->span_n)
@@ -1711,6 +1796,7 @@ int pbgpu_kernel_times(pbgpu_ctx *ctx, double *ms_each, uint32_t cap, uint32_t *
     if (ctx == NULL || (cap && ms_each == NULL))
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
     uint32_t n = 0;
     for (auto &p : ctx->pending)
     {
@@ -1733,6 +1819,7 @@ int pbgpu_fill_probe_ex(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *m
     if (ctx == NULL || bytes < 16 || reps == 0)
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
     void *buf = NULL;
     HIPCHK(hipMalloc(&buf, bytes));
     hipEvent_t a, b;
@@ -1801,8 +1888,6 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
-    else if (K.sw_nw)
-        snprintf(buf, n, "pb_swin_kernel<%u, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
     else if (K.xs_np && !env_is("PBGPU_KERNEL", "linear"))
         snprintf(buf, n, "%s<%u, %u, %s>", K.xp ? "pb_xpage_kernel" : "pb_xsmall_kernel", K.small_ndw, K.proto,
                  K.pl0.random ? "true" : "false");

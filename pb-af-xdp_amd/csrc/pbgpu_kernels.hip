@@ -536,62 +536,6 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
         pb_count(K, blockIdx.x, nfr, tile_bytes);
 }
 
-// Windowed form (the 98-B ICMP and 106-B UDP frames of configs[4] / configs[0], every other fixed
-// length <= 128 B that pb_xsmall_kernel / pb_xpage_kernel do not take): a workgroup owns a
-// region of NW windows of 256 frames (XCD-contiguous regions, pb_xcd_region) and builds them one
-// window at a time — one lane per frame into the LDS tile, a barrier, the window's bytes out as
-// 16-B stores whose absolute chunk index is the lane (each wave store one 1-KiB-aligned block),
-// a barrier.  The linear form's 64-frame (6 KiB) workgroups write the 64-thread-workgroup store
-// shape (<= 6.4 TB/s in profiles/r02/wbench), where a long region walked in order by each XCD
-// reaches the staged 1500-B kernel's 6.6-7.0 TB/s.  256 frames of even length end on a 128-B
-// line, so no line has two writers.
-template <int NDW, int PROTO, bool RANDOM>
-__global__ __launch_bounds__(PB_WG) void pb_swin_kernel(pb_kargs K)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t s_tile[PB_WG * NDW + 8];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t nw = K.sw_nw;
-    const uint32_t bxr = pb_xcd_region(blockIdx.x, gridDim.x);
-    const uint32_t flen = K.fixed_len;
-    const uint64_t fr0 = (uint64_t)bxr * nw * PB_WG;
-    const bool swz = (flen & 7u) == 0;
-    uint32_t built = 0;
-    for (uint32_t w = 0; w < nw; ++w)
-    {
-        const uint64_t f0 = fr0 + (uint64_t)w * PB_WG;
-        if (f0 >= K.n_frames)
-            break;
-        const uint64_t left = K.n_frames - f0;
-        const uint32_t nfr = left < PB_WG ? (uint32_t)left : PB_WG;
-        if (tid < nfr)
-        {
-            uint32_t d[NDW];
-            pb_small_frame<NDW, PROTO, RANDOM>(K, f0 + tid, d);
-            pb_small_put<NDW>(s_tile, d, tid * flen, flen);
-        }
-        __syncthreads();
-        const uint32_t tile_bytes = nfr * flen;
-        const uint32_t nchunks = (tile_bytes + 15) >> 4;
-        const uint64_t ob = f0 * flen; // 16-B aligned (256 frames of any length are)
-        uint8_t *const out = K.out + ob;
-        for (uint32_t c = (tid - (uint32_t)(ob >> 4)) & (PB_WG - 1u); c < nchunks; c += PB_WG)
-        {
-            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[swz ? pb_swz(c) : c];
-            if (16 * c + 16 > tile_bytes) // last chunk of the stream: zero the tail
-            {
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    v[t] &= pb_range_mask(0, (int)tile_bytes - (int)(16 * c + 4 * t));
-            }
-            pb_st16(out + 16 * c, v);
-        }
-        built += nfr;
-        __syncthreads(); // the next window reuses the tile
-    }
-    if (tid == 0)
-        pb_count(K, bxr, built, (uint64_t)built * flen);
-}
-
 // XCD-owned form, for frame lengths that divide 4096 (64-B configs[1] frames,
 // 128-B frames).  The output stream (4 KiB aligned) is cut into 4 KiB pages of
 // fp = 4096 / flen whole frames; workgroup b, which the dispatcher deals to XCD
@@ -707,6 +651,7 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
     // 512-thread workgroup, two unrolled passes per 256-thread one (a loop kept the
     // kernel arguments live across iterations and spilled them through v_readlane /
     // v_writelane, 41 VALU per frame)
+    uint32_t starts = 0; // this lane's frames that start in their page (the counters)
 #pragma unroll
     for (uint32_t pass = 0; pass < 512 / WGT; ++pass)
     {
@@ -729,12 +674,20 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
         uint32_t d[NDW];
         pb_small_frame<NDW, PROTO, RANDOM>(K, f, d, rtab);
         const int off = (int)((int64_t)(f * flen) - (int64_t)p0); // (-flen, 4096), dword aligned
+        starts += off >= 0 ? 1u : 0u;
         uint32_t *row = s_tile + (i * PB_XREG + 128 + off) / 4;
 #pragma unroll
         for (int t = 0; t < NDW; ++t)
             if ((uint32_t)(4 * t) < flen)
                 row[t] = d[t];
     }
+    // per-wave sums of the frame starts (no init race: one plain write per wave)
+    __shared__ uint32_t s_starts[WGT / 64];
+#pragma unroll
+    for (uint32_t dd = 32; dd > 0; dd >>= 1)
+        starts += __shfl_xor(starts, dd, 64);
+    if ((tid & 63u) == 0)
+        s_starts[tid >> 6] = starts;
     __syncthreads();
 
     // page i -> HBM: one 16-B store per lane per page (256 lanes per page)
@@ -757,17 +710,16 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
     }
     if (tid == 0)
     {
-        // the stored pages, and the frames that start in them (each frame counted once)
+        // the stored pages, and the frames that start in them (each frame counted once; summed
+        // from the building lanes: 64-bit divisions here on one lane cost the kernel ~45%)
         uint64_t fr = 0, by = 0;
+        for (uint32_t w = 0; w < WGT / 64; ++w)
+            fr += s_starts[w];
         for (uint32_t i = 0; i < np; ++i)
         {
             const uint32_t c = c0 + i * cs;
-            if (c >= K.xs_nch)
-                continue;
-            const uint64_t p0 = (uint64_t)c * PB_XPG;
-            by += min((uint64_t)PB_XPG, T - p0);
-            const uint64_t fa = (p0 + flen - 1) / flen, fb = min(K.n_frames, (p0 + PB_XPG + flen - 1) / flen);
-            fr += fb > fa ? fb - fa : 0;
+            if (c < K.xs_nch)
+                by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
         }
         pb_count(K, b, fr, by);
     }
@@ -2710,15 +2662,7 @@ __global__ __launch_bounds__(256) void pb_fillreg_kernel(pb_u32x4 *dst, uint64_t
 template <int NDW, int PROTO>
 static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
 {
-    if (K->sw_nw && !K->xs_grid)
-    {
-        const uint32_t g = (uint32_t)((K->n_frames + (uint64_t)K->sw_nw * PB_WG - 1) / ((uint64_t)K->sw_nw * PB_WG));
-        if (K->pl0.random)
-            hipLaunchKernelGGL((pb_swin_kernel<NDW, PROTO, true>), dim3(g), dim3(PB_WG), K->lds_pad, st, *K);
-        else
-            hipLaunchKernelGGL((pb_swin_kernel<NDW, PROTO, false>), dim3(g), dim3(PB_WG), K->lds_pad, st, *K);
-    }
-    else if (K->xs_grid && K->xp)
+    if (K->xs_grid && K->xp)
     {
         const size_t lds = (size_t)K->xs_np * PB_XREG + K->lds_pad;
         const bool w512 = K->xp_wgt == 512;

@@ -148,9 +148,8 @@ XS_LENS = [42, 43, 44, 48, 52, 56, 60, 64, 72, 96, 98, 100, 106, 108, 116, 120, 
 XS_COUNTS = [1, 5, 200, 2048, 2049, 2 * 2048 * 5 + 77]
 
 
-@pytest.mark.parametrize("force_xpage", [False, True, 512, "lin64", "lin128", "win1", "win4"],
-                         ids=["default", "xpage_forced", "xpage_forced_512", "linear_wg64", "linear_wg128",
-                              "windows_1", "windows_4"])
+@pytest.mark.parametrize("force_xpage", [False, True, 512, "lin64", "lin128"],
+                         ids=["default", "xpage_forced", "xpage_forced_512", "linear_wg64", "linear_wg128"])
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
 @pytest.mark.parametrize("flen", XS_LENS)
 def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
@@ -163,11 +162,6 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
         monkeypatch.delenv("PBGPU_XP_FORCE", raising=False)
         monkeypatch.setenv("PBGPU_KERNEL", "linear")
         monkeypatch.setenv("PBGPU_SMALL_WGT", force_xpage[3:])
-    win = force_xpage in ("win1", "win4")
-    if win:  # the windowed small kernel (pb_swin_kernel) for every length
-        monkeypatch.delenv("PBGPU_XP_FORCE", raising=False)
-        monkeypatch.setenv("PBGPU_KERNEL", "linear")
-        monkeypatch.setenv("PBGPU_SMALL_WIN", force_xpage[3:])
     hl = 54 if proto == "tcp" else 42
     if flen < hl or (proto == "icmp" and flen == hl):
         pytest.skip("shorter than the headers / empty static payload")
@@ -180,9 +174,7 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
         n = max(1, n * 64 // flen)  # page counts as named above at every length
         kern = _check(ctx, cfg, 1000003 + n, n)
         xp_default = flen <= 64 and 512 // ((4096 + flen - 1) // flen + 1) >= 6
-        if win:
-            want = "pb_swin_kernel<"
-        elif lin:
+        if lin:
             want = "pb_small_kernel<"
         elif flen % 4 == 0 and (force_xpage or (4096 % flen and xp_default)):
             want = "pb_xpage_kernel"

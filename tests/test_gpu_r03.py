@@ -135,3 +135,40 @@ def test_binary_draws_a_seed_per_run_unless_given(tmp_path):
     replay = sa.split("--seed ")[1].rstrip(").")
     e, _ = run("e", "--seed", replay)
     assert e == a
+
+
+# span timing: each sequence builds on a stream of its own, so the kernels of different
+# sequences overlap; a buffer rebuilt by another sequence, the counters, the span and the
+# copies must still see every build in order
+def test_sequence_streams_build_the_same_bytes(ctx):
+    names = ["c2_udp_64", "c4_tcp_syn", "c5_icmp_echo", "c3_udp_var"]
+    n = 5000
+    seqs = [Sequence.from_config(pc.get(nm)) for nm in names]
+    for i, s in enumerate(seqs):
+        ctx.load_sequence(4 + i, s, pc.SEED_BASE)
+    cap = [ctx.build_size(4 + i, n) for i in range(len(names))]
+    shared = ctx.alloc_frames(max(c[0] for c in cap), max(c[1] for c in cap))
+    bufs = [ctx.alloc_frames(*c) for c in cap]
+    ctx.set_timing(ctx.TIMING_SPAN)
+    try:
+        p0, b0 = ctx.counters(4 + len(names))
+        for rep in range(3):
+            for i in range(len(names)):
+                ctx.build(4 + i, 100 + rep * n, n, bufs[i])
+        # one buffer built by every sequence in turn, last by the variable-length one
+        for i in range(len(names)):
+            ctx.build(4 + i, 77, n, shared)
+        ms, k = ctx.kernel_time()
+        assert k == 3 * len(names) + len(names) and ms > 0
+        p1, b1 = ctx.counters(4 + len(names))
+        for i, s in enumerate(seqs):
+            data, off = bufs[i].packed(), bufs[i].offsets()
+            o_data, o_off = ob.build(s, 4 + i, 100 + 2 * n, n, pc.SEED_BASE)
+            assert np.array_equal(off, o_off) and np.array_equal(data, o_data), names[i]
+            assert int(p1[4 + i] - p0[4 + i]) == 4 * n
+        o_data, o_off = ob.build(seqs[-1], 4 + len(names) - 1, 77, n, pc.SEED_BASE)
+        assert np.array_equal(shared.offsets(), o_off) and np.array_equal(shared.packed(), o_data)
+    finally:
+        ctx.set_timing(ctx.TIMING_LAUNCH)
+        for b in bufs + [shared]:
+            b.free()
