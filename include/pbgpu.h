@@ -55,7 +55,12 @@ typedef struct pbgpu_ctx pbgpu_ctx;
  *   fixed_len > 0 : offset(f) = f * fixed_len, len(f) = fixed_len
  *   fixed_len == 0: offset(f) = offsets[f], len(f) = offsets[f+1] - offsets[f]
  * Frames are numbered iteration-major: f = (k - first_iter) * pl_cnt + i for
- * payload i of iteration k (the reference's inner loop, sequence.c:530). */
+ * payload i of iteration k (the reference's inner loop, sequence.c:530).
+ * Variable length: offsets[n_frames] (the total) is written by every build; the
+ * packed-frame kernel writes the other offsets as 4-B low words plus one 8-B start
+ * per workgroup region, and offsets[] is filled from them on first use —
+ * pbgpu_copy_offsets(), pbgpu_copy_to_umem[_async]() — or by pbgpu_frames_offsets()
+ * for a caller that reads offsets[] on the device itself. */
 typedef struct pbgpu_frames
 {
     uint8_t *data;          /* device pointer, capacity_bytes (16-B padded) */
@@ -105,6 +110,9 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
 
 int pbgpu_sync(pbgpu_ctx *ctx);
 int pbgpu_frames_total(pbgpu_ctx *ctx, pbgpu_frames *frames, uint64_t *total_bytes);
+/* Fills offsets[0 .. n_frames) of a variable-length build (ordered on the context's
+ * stream; a no-op when they are already there). */
+int pbgpu_frames_offsets(pbgpu_ctx *ctx, pbgpu_frames *frames);
 
 /* ---- landing: device -> host ---- */
 int pbgpu_copy_packed(pbgpu_ctx *ctx, const pbgpu_frames *frames, void *host_dst,

@@ -148,6 +148,10 @@ struct pb_kargs
     uint32_t vl_wgf;        // its own frames per workgroup (<= 256 - PB_VST_GHOSTS)
     uint32_t vl_nl48;       // lcg48 entries it keeps in LDS (chunks of the longest frame + 2)
     uint32_t vl_nlines;     // its line-map entries (128-B lines of the longest workgroup region)
+    // pb_vline_kernel: 4-B offsets (the low word of each frame's offset) and each workgroup
+    // region's 64-bit start, instead of 8-B offsets; pbgpu.cpp expands them on first use
+    uint32_t *offsets32;
+    unsigned long long *vl_rstart;
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

@@ -28,6 +28,8 @@ extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *
                                          uint64_t *offsets, hipStream_t st);
 extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t wgf, uint32_t *bsum, uint32_t nblk,
                                              unsigned long long *l2, uint32_t n_l2, uint64_t *offsets, hipStream_t st);
+extern "C" hipError_t pbk_launch_expand_offsets(const uint32_t *off32, const unsigned long long *rstart, uint32_t wf,
+                                                uint64_t n, uint64_t *offsets, hipStream_t st);
 extern "C" hipError_t pbk_launch_scatter(const uint8_t *src, const uint64_t *offsets, uint64_t first, uint32_t n,
                                          uint8_t *dst, uint32_t stride, uint16_t *lens, hipStream_t st);
 extern "C" hipError_t pbk_launch_fill(void *dst, uint64_t bytes, int mode, hipStream_t st);
@@ -120,6 +122,12 @@ struct frames_events
     bool land_pending = false;
     hipStream_t last = nullptr; // the stream the buffer was last built on
     hipEvent_t moved = nullptr; // a build on another stream waits on this (recorded on `last`)
+    // pb_vline_kernel writes 4-B offsets and region starts here; offsets[] is expanded from them
+    // on first use (packed32 set until then)
+    uint32_t *d_off32 = nullptr;
+    unsigned long long *d_rstart = nullptr;
+    bool packed32 = false;
+    uint32_t wf = 0;
 };
 
 frames_events *frames_ev(pbgpu_frames *f)
@@ -1175,6 +1183,10 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
             (void)hipEventDestroy(fe->built);
         if (fe->moved)
             (void)hipEventDestroy(fe->moved);
+        if (fe->d_off32)
+            (void)hipFree(fe->d_off32);
+        if (fe->d_rstart)
+            (void)hipFree(fe->d_rstart);
         if (fe->landed)
             (void)hipEventDestroy(fe->landed);
         delete fe;
@@ -1251,6 +1263,30 @@ static int mark_built(pbgpu_ctx *ctx, pbgpu_frames *out, hipStream_t st)
     return PBGPU_OK;
 }
 
+// offsets[] of a build that wrote 4-B offsets, expanded on the context's stream (after the
+// sequence streams are joined); later builds of the buffer follow it (fe->last)
+static int materialize_offsets(pbgpu_ctx *ctx, const pbgpu_frames *f)
+{
+    frames_events *fe = (frames_events *)f->reserved;
+    if (fe == NULL || !fe->packed32)
+        return PBGPU_OK;
+    PB_JOIN(ctx);
+    HIPCHK(pbk_launch_expand_offsets(fe->d_off32, fe->d_rstart, fe->wf, f->n_frames, f->offsets, ctx->stream));
+    fe->packed32 = false;
+    fe->last = ctx->stream;
+    if (fe->built) // a landing waits for the expansion too
+        HIPCHK(hipEventRecord(fe->built, ctx->stream));
+    return PBGPU_OK;
+}
+
+int pbgpu_frames_offsets(pbgpu_ctx *ctx, pbgpu_frames *f)
+{
+    if (ctx == NULL || f == NULL)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    return materialize_offsets(ctx, f);
+}
+
 int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, pbgpu_frames *out)
 {
     if (ctx == NULL || out == NULL || seq_idx >= PB_MAX_SEQUENCES)
@@ -1292,6 +1328,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         HIPCHK(hipStreamWaitEvent(st, fe->moved, 0));
     }
     fe->last = st;
+    fe->packed32 = false;
     // a landing queued from this buffer must have read it before the build overwrites it
     if (fe->land_pending)
     {
@@ -1337,6 +1374,19 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             K.vblk_sum = bsum;
             K.vblk_l2 = l2;
             K.offsets_w = out->offsets;
+            if (K.vl)
+            {
+                // 4 B per frame and 8 B per region instead of 8 B per frame
+                if (fe->d_off32 == nullptr)
+                {
+                    HIPCHK(hipMalloc((void **)&fe->d_off32, (out->capacity_frames + 1) * sizeof(uint32_t)));
+                    HIPCHK(hipMalloc((void **)&fe->d_rstart, (out->capacity_frames / 32 + 2) * sizeof(unsigned long long)));
+                }
+                K.offsets32 = fe->d_off32;
+                K.vl_rstart = fe->d_rstart;
+                fe->packed32 = true;
+                fe->wf = wgf;
+            }
         }
         else
         {
@@ -1476,6 +1526,11 @@ int pbgpu_copy_offsets(pbgpu_ctx *ctx, const pbgpu_frames *f, uint64_t *dst)
         return PBGPU_OK;
     }
     PB_JOIN(ctx);
+    {
+        const int mrc = materialize_offsets(ctx, f);
+        if (mrc != PBGPU_OK)
+            return mrc;
+    }
     HIPCHK(hipMemcpyAsync(dst, f->offsets, (f->n_frames + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
                           ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1629,6 +1684,12 @@ int pbgpu_copy_to_umem_async(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, 
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
     PB_JOIN(ctx);
+    if (!f->fixed_len)
+    {
+        const int mrc = materialize_offsets(ctx, f);
+        if (mrc != PBGPU_OK)
+            return mrc;
+    }
     hipStream_t ls = ctx->land_stream;
     ctx->land_events = true;
     frames_events *fe = (frames_events *)f->reserved;

@@ -2289,8 +2289,12 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         S0 += s_st0[8 + w];
     const uint64_t base0 = S0 - s_st0[GH]; // start of slot 0
     const uint64_t start = base0 + pre + (inc - flen);
-    if (valid && tid >= GH) // own frames: the offsets
-        K.offsets_w[(uint64_t)fj] = start;
+    if (valid && tid >= GH) // own frames: the offsets' low words, the region's start
+    {
+        K.offsets32[(uint64_t)fj] = (uint32_t)start;
+        if (tid == GH)
+            K.vl_rstart[bxr] = start;
+    }
     // region [lo, hi): lo = the 128-B line of the first own frame's start (0 for the first region),
     // hi = the next region's lo (the launch's end for the last)
     const bool last = fe == K.n_frames;
@@ -2923,6 +2927,26 @@ extern "C" hipError_t pbk_launch_scatter_fixed(const uint8_t *src, uint32_t flen
     const uint64_t n_dw = (uint64_t)n * dpf;
     hipLaunchKernelGGL(pb_scatter_fixed, dim3((uint32_t)((n_dw + 255) / 256)), dim3(256), 0, st, src, flen, dpf, n_dw,
                        dst, stride);
+    return hipGetLastError();
+}
+
+// offsets[f] from pb_vline_kernel's 32-bit low words: region r = f / wf starts at rstart[r] and
+// spans < 2^32 bytes, so the frame's offset is rstart[r] plus the 32-bit difference of low words.
+__global__ __launch_bounds__(256) void pb_expand_offsets(const uint32_t *off32, const unsigned long long *rstart,
+                                                         uint32_t wf, uint64_t n, uint64_t *offsets)
+{
+    const uint64_t f = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (f >= n)
+        return;
+    const unsigned long long r0 = rstart[(uint32_t)f / wf];
+    offsets[f] = r0 + (uint32_t)(off32[f] - (uint32_t)r0);
+}
+
+extern "C" hipError_t pbk_launch_expand_offsets(const uint32_t *off32, const unsigned long long *rstart, uint32_t wf,
+                                                uint64_t n, uint64_t *offsets, hipStream_t st)
+{
+    hipLaunchKernelGGL(pb_expand_offsets, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, off32, rstart, wf, n,
+                       offsets);
     return hipGetLastError();
 }
 

@@ -34,6 +34,7 @@ enum
     OPT_PCAP,
     OPT_TX,
     OPT_VERYRANDOM,
+    OPT_UMEMFRAMES,
 };
 
 static const struct option af_xdp_opts[] = {
@@ -53,6 +54,7 @@ static const struct option af_xdp_opts[] = {
     {"pcap", required_argument, NULL, OPT_PCAP},
     {"tx", required_argument, NULL, OPT_TX},
     {"veryrandom", no_argument, NULL, OPT_VERYRANDOM},
+    {"umemframes", required_argument, NULL, OPT_UMEMFRAMES},
     {NULL, 0, NULL, 0},
 };
 
@@ -63,6 +65,7 @@ void cmd_line_af_xdp_defaults(struct cmd_line_af_xdp *c)
     c->gpu_first = 0;
     c->gpu_batch = 1u << 20;
     c->seed_base = 0x5EEDBA5Eull;
+    c->umem_frames = 4096; /* NUM_FRAMES, af_xdp.h:23 */
 }
 
 void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *c, int argc, char **argv)
@@ -123,6 +126,9 @@ void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *c, int argc, char **argv)
         case OPT_VERYRANDOM:
             c->very_random = 1;
             break;
+        case OPT_UMEMFRAMES:
+            c->umem_frames = (uint32_t)strtoul(optarg, NULL, 0);
+            break;
         default:
             break;
         }
@@ -134,6 +140,11 @@ int pb_af_xdp_setup(const struct cmd_line_af_xdp *c, int verbose)
     if (c->skb_mode && c->zero_copy)
     {
         fprintf(stderr, "--skb and --zerocopy cannot be combined: SKB (generic XDP) mode sends in copy mode.\n");
+        return -EINVAL;
+    }
+    if (c->umem_frames < 64 || c->umem_frames > (1u << 20) || (c->umem_frames & (c->umem_frames - 1)))
+    {
+        fprintf(stderr, "--umemframes must be a power of two from 64 to 1048576.\n");
         return -EINVAL;
     }
     if (c->batch_set && c->batch_size == 0)

@@ -28,7 +28,7 @@
 
 #define PB_MAX_WORKERS 1024
 #define PB_LAND_INFLIGHT_MAX 16 /* landings queued per thread (PB_LAND_INFLIGHT, default 2) */
-#define PB_LAND_CHUNK_DEF 2048   /* frames per landing (PB_LAND_CHUNK; half of the UMEM) */
+/* frames per landing: half of the UMEM (PB_LAND_CHUNK overrides) */
 
 static uint32_t env_u32(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi)
 {
@@ -296,12 +296,19 @@ static void *gpu_worker(void *p)
     memset(&xsk, 0, sizeof xsk);
     xsk.fd = -1;
     sink_arg_t sink = {w->shard, seq_num};
-    /* this thread's UMEM slots: its own NUM_FRAMES, or its range of the sequence's shared UMEM */
-    const uint32_t nslots = w->shared ? w->shared->slots : PB_NUM_FRAMES;
+    /* this thread's UMEM slots: its own NUM_FRAMES (--umemframes), or its range of the
+     * sequence's shared UMEM */
+    const uint32_t umem_frames = w->cmd.umem_frames ? w->cmd.umem_frames : PB_NUM_FRAMES;
+    const uint32_t nslots = w->shared ? w->shared->slots : umem_frames;
     const uint32_t slot_base = w->shared ? (uint32_t)w->shard * nslots : 0;
     const size_t umem_bytes = (size_t)nslots * PB_FRAME_SIZE;
-    uint16_t lens[PB_NUM_FRAMES];
+    uint16_t *lens = (uint16_t *)calloc(nslots, sizeof(uint16_t));
     int rc;
+    if (lens == NULL)
+    {
+        last_error = PBGPU_ENOMEM;
+        goto out;
+    }
 
     if ((rc = B->open(w->gpu, &ctx)) != 0)
     {
@@ -415,7 +422,7 @@ static void *gpu_worker(void *p)
             }
         }
         rc = pb_xsk_open(&xsk, w->device, q, umem_base, nslots, PB_FRAME_SIZE, bf, shared_fd, slot_base,
-                         w->shared ? (uint32_t)PB_NUM_FRAMES : nslots);
+                         w->shared ? umem_frames : nslots);
         if (w->shared && w->shard == 0)
         {
             pthread_mutex_lock(&w->shared->mu);
@@ -449,7 +456,7 @@ static void *gpu_worker(void *p)
 
     /* landing granularity: frames per landing and landings in flight (their launch and
      * completion latencies overlap); tunable for the host-rate probe (scripts/e2e_probe.py) */
-    const uint32_t land_chunk = env_u32("PB_LAND_CHUNK", PB_LAND_CHUNK_DEF, 1, nslots);
+    const uint32_t land_chunk = env_u32("PB_LAND_CHUNK", nslots / 2 > 0 ? nslots / 2 : 1, 1, nslots);
     /* 64-B UDP, one TX thread (profiles/r03/e2e): 2048 x 2 129-137 Mpps, 1024 x 3 73, 512 x 6 34-43,
      * 256 x 12 20-28 — each landing is a kernel launch and a host wait, so few large ones win */
     const uint32_t land_inflight = env_u32("PB_LAND_INFLIGHT", 2, 1, PB_LAND_INFLIGHT_MAX);
@@ -663,6 +670,7 @@ out:
             B->free_frames(ctx, fr[i]);
     if (ctx)
         B->close(ctx);
+    free(lens);
     free(w);
     return NULL;
 }
@@ -693,26 +701,27 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
     {
         /* one UMEM for the sequence's threads (af_xdp.c:412-428), each its own power-of-two
          * slot range */
-        uint32_t slots = PB_NUM_FRAMES;
-        while (slots > 1 && slots * (uint32_t)t_cnt > PB_NUM_FRAMES)
+        const uint32_t umem_frames = cmd.umem_frames ? cmd.umem_frames : PB_NUM_FRAMES;
+        uint32_t slots = umem_frames;
+        while (slots > 1 && slots * (uint32_t)t_cnt > umem_frames)
             slots >>= 1;
-        if (slots * (uint32_t)t_cnt > PB_NUM_FRAMES)
+        if (slots * (uint32_t)t_cnt > umem_frames)
         {
-            fprintf(stderr, "[%d] Too many threads (%d) for one shared UMEM of %d frames.\n", idx + 1, t_cnt,
-                    PB_NUM_FRAMES);
+            fprintf(stderr, "[%d] Too many threads (%d) for one shared UMEM of %u frames.\n", idx + 1, t_cnt,
+                    umem_frames);
             last_error = PBGPU_EINVAL;
             return;
         }
         shared = (shared_umem_t *)calloc(1, sizeof *shared);
         if (shared == NULL ||
             posix_memalign((void **)&shared->base, (size_t)sysconf(_SC_PAGESIZE),
-                           (size_t)PB_NUM_FRAMES * PB_FRAME_SIZE) != 0)
+                           (size_t)umem_frames * PB_FRAME_SIZE) != 0)
         {
             free(shared);
             last_error = PBGPU_ENOMEM;
             return;
         }
-        memset(shared->base, 0, (size_t)PB_NUM_FRAMES * PB_FRAME_SIZE);
+        memset(shared->base, 0, (size_t)umem_frames * PB_FRAME_SIZE);
         shared->slots = slots;
         shared->fd = -1;
         shared->refs = 1; /* seq_send's own reference, dropped after the threads are started */

@@ -274,6 +274,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pbgpu_build": (C.c_int, [P, C.c_uint16, C.c_uint64, C.c_uint64, FP]),
         "pbgpu_sync": (C.c_int, [P]),
         "pbgpu_frames_total": (C.c_int, [P, FP, U64P]),
+        "pbgpu_frames_offsets": (C.c_int, [P, FP]),
         "pbgpu_copy_packed": (C.c_int, [P, FP, P, C.c_uint64, C.c_uint64]),
         "pbgpu_copy_offsets": (C.c_int, [P, FP, U64P]),
         "pbgpu_copy_to_umem": (C.c_int, [P, FP, P, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32,
@@ -291,6 +292,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pbgpu_kernel_name": (C.c_int, [P, C.c_uint16, C.c_char_p, C.c_size_t]),
     }
     for name, (res, args) in sig.items():
+        if path != LIB_PATH and not hasattr(lib, name):
+            continue  # an older build loaded for an A/B lacks the newer entry points
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -324,6 +327,10 @@ class FrameBuffer:
         t = C.c_uint64()
         _check(self.ctx.lib.pbgpu_frames_total(self.ctx.h, self.ptr, C.byref(t)), "frames_total")
         return int(t.value)
+
+    def fill_offsets(self) -> None:
+        """offsets[] on the device (variable length: expanded from the 4-B form on first use)."""
+        _check(self.ctx.lib.pbgpu_frames_offsets(self.ctx.h, self.ptr), "frames_offsets")
 
     def offsets(self) -> np.ndarray:
         n = int(self.f.n_frames)

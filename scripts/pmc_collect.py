@@ -23,7 +23,7 @@ for d in sorted(glob.glob(os.path.join(out_dir, "pmc_*"))):
         agg = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"]
-            build = kn.startswith("void pb_") and ("gpf" in kn or "stage" in kn or "small" in kn or "xpage" in kn)
+            build = kn.startswith("void pb_") and any(x in kn for x in ("gpf", "stage", "small", "xpage", "vline"))
             aux = kn.startswith("void pb_len_") or kn.startswith("pb_len_") or "pb_scan_blocks" in kn
             if not (build or aux):
                 continue

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round-3 profile evidence: the GPU suite and smoke, a rocprofv3 kernel trace + stats of the
+# default bench command, separate --pmc passes (WRITE_SIZE / FETCH_SIZE / SQ / LDS) per BASELINE
+# config, and one bench line per config whose roofline.traffic comes from those passes
+# (profiles/pmc_r03.json).  Output: gpurun_out/prof_r03/.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_r03
+rm -rf $OUT; mkdir -p $OUT/cfg
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?
+echo "rc=$rc" >> $OUT/pytest.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench_trace -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-seconds 2 > $OUT/bench_trace.log 2>&1 || { echo TRACE_FAIL; tail -5 $OUT/bench_trace.log; exit 1; }
+grep '^{"metric"' $OUT/bench_trace.log > $OUT/bench_under_trace.json
+python3 scripts/trace_summary.py $OUT/bench_trace/run_kernel_trace.csv $OUT/kernel_trace_summary.json
+echo "trace done"
+for cfg in c2_udp_64 c2_udp_1500 c3_udp_var c4_tcp_syn c5_icmp_echo; do
+  B="python3 bench.py --steps 5 --warmup 2 --ramp-seconds 0 --no-variants --cpu-seconds 0 --config $cfg --packets 33554432"
+  for grp in "WRITE_SIZE" "FETCH_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
+    tag=$(echo $grp | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+    timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_${cfg}_$tag -o run -- $B > $OUT/pmc_${cfg}_$tag.log 2>&1 || { echo "PMC_FAIL $cfg $grp"; tail -3 $OUT/pmc_${cfg}_$tag.log; exit 1; }
+  done
+  echo "pmc done $cfg"
+done
+python3 scripts/pmc_collect.py $OUT
+cp $OUT/pmc_summary.json profiles/pmc_r03.json
+for cfg in c2_udp_64 c2_udp_1500 c3_udp_var c4_tcp_syn c5_icmp_echo c5_mix; do
+  V=--no-variants; [ $cfg = c3_udp_var ] && V=
+  timeout -k 10 200 python3 bench.py --steps 50 --warmup 5 $V --cpu-seconds 0 --config $cfg --pmc profiles/pmc_r03.json > $OUT/cfg/$cfg.json || exit 1
+  python3 -c "import json; d=json.load(open('$OUT/cfg/$cfg.json')); r=d['roofline']; print('$cfg', r['kernel'], r['kernel_ms_avg'], r['achieved'], 'GB/s', r['frac'], d['write_peak_probe_gbps'], r['traffic'])"
+done

@@ -172,3 +172,23 @@ def test_sequence_streams_build_the_same_bytes(ctx):
         ctx.set_timing(ctx.TIMING_LAUNCH)
         for b in bufs + [shared]:
             b.free()
+
+
+# pb_vline_kernel writes 4-B offsets and region starts; offsets[] is expanded on first use and
+# must follow every rebuild of the buffer (a stale expansion would keep the first build's)
+def test_packed_offsets_expand_after_every_build(ctx):
+    seq = Sequence.from_config(pc.get("c3_udp_var"))
+    ctx.load_sequence(9, seq, pc.SEED_BASE)
+    n = 3001
+    fb = ctx.alloc_frames(*ctx.build_size(9, n))
+    try:
+        assert ctx.kernel_name(9).startswith("pb_vline_kernel")
+        for first in (5, 123457, 5):
+            ctx.build(9, first, n, fb)
+            fb.fill_offsets()
+            fb.fill_offsets()  # a second call is a no-op
+            o_data, o_off = ob.build(seq, 9, first, n, pc.SEED_BASE)
+            assert np.array_equal(fb.offsets(), o_off)
+            assert np.array_equal(fb.packed(), o_data)
+    finally:
+        fb.free()
