@@ -2,7 +2,8 @@
 descriptors on the in-memory ring, no pcap) for one case under several
 environment variants (landing chunk / landings in flight / spin waits, or any
 library switch).  Steady rate = 3N / (t(4N) - t(N)), as scripts/e2e_probe.py.
-python3 e2e_ab.py CASE THREADS 'tag:VAR=a,VAR2=b' ...   CASE: udp64 | udp1500 | var"""
+python3 e2e_ab.py CASE THREADS 'tag:VAR=a,VAR2=b' ...   CASE: udp64 | udp1500 | var
+(ARGS=... in a variant appends command-line arguments.)"""
 import json
 import os
 import re
@@ -18,9 +19,9 @@ BASE = ["-z", "--interface", "pbnodev0", "--smac", "52:54:00:59:29:cc", "--dmac"
 CASES = {"udp64": (22, 22, 1 << 24), "udp1500": (1458, 1458, 1 << 21), "var": (64, 1500, 1 << 22)}
 
 
-def run(env, lo, hi, n, threads, batch):
+def run(env, lo, hi, n, threads, batch, extra=()):
     cmd = [BIN] + BASE + ["--pmin", str(lo), "--pmax", str(hi), "--maxpckts", str(n), "--threads", str(threads),
-                          "--gpubatch", str(batch)]
+                          "--gpubatch", str(batch)] + list(extra)
     t0 = time.perf_counter()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     dt = time.perf_counter() - t0
@@ -41,8 +42,9 @@ for rep in range(int(os.environ.get("REPS", "2"))):
     for tag, extra in variants:
         env = dict(os.environ, PB_SEQ_GAP_MS="0", **extra)
         batch = int(extra.get("GPUBATCH", 1 << 18))
-        p1, b1, t1 = run(env, lo, hi, n, threads, batch)
-        p4, b4, t4 = run(env, lo, hi, 4 * n, threads, batch)
+        args = extra.get("ARGS", "").split()  # extra command-line arguments ('ARGS=--umemframes 16384')
+        p1, b1, t1 = run(env, lo, hi, n, threads, batch, args)
+        p4, b4, t4 = run(env, lo, hi, 4 * n, threads, batch, args)
         slope = t4 - t1
         print(json.dumps({"case": case, "tag": tag, "env": extra, "threads": threads, "rep": rep,
                           "steady_mpps": round((p4 - p1) / slope / 1e6, 1),

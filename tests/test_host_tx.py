@@ -444,3 +444,21 @@ def test_seed_is_drawn_per_run_unless_given(libs):
     assert host.pb_resolve_seed(C.byref(r1)) != host.pb_resolve_seed(C.byref(r2))
     s1, s2 = _cmd(host, seed_base=1234, seed_set=1), _cmd(host, seed_base=1234, seed_set=1)
     assert host.pb_resolve_seed(C.byref(s1)) == host.pb_resolve_seed(C.byref(s2)) == 1234
+
+
+@pytest.mark.parametrize("umem_frames,shared,threads", [(64, 0, 1), (16384, 0, 2), (16384, 1, 4)])
+def test_umemframes_sizes_each_umem(libs, umem_frames, shared, threads):
+    """--umemframes N: UMEM slots per socket (the reference's NUM_FRAMES, af_xdp.h:23, is
+    4096); landings take half of them at a time.  Exact quota, every frame once and intact,
+    with private and shared UMEMs."""
+    r = _run(libs, _cfg(0, 900, maxpckts=60000, delay=0, threads=threads), gpu_batch=20000,
+             umem_frames=umem_frames, shared_umem=shared)
+    assert r["err"] == 0 and r["pckts"] == 60000 and r["seen"] == 60000
+    assert len(np.unique(r["k"])) == 60000 and (r["len"] != 0xFFFF).all()
+
+
+def test_umemframes_must_be_a_power_of_two(libs):
+    host = libs[0]
+    host.pb_af_xdp_setup.argtypes = [C.POINTER(OurCmd), C.c_int]
+    for n, ok in ((4096, True), (64, True), (1 << 20, True), (1000, False), (32, False), (1 << 21, False)):
+        assert (host.pb_af_xdp_setup(C.byref(_cmd(host, umem_frames=n)), 0) == 0) == ok, n
