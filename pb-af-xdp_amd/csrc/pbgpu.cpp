@@ -163,6 +163,8 @@ struct pbgpu_ctx
     // kernels of different sequences overlap (as the reference's non-blocking sequences run
     // their threads side by side, sequence.c:741-765); every other call first joins them
     // into `stream` (one event per stream that built since the last join)
+    // counts of a slot's earlier sequences (folded in when the slot is loaded again)
+    uint64_t ctr_base[PB_MAX_SEQUENCES][2] = {};
     hipStream_t seq_stream[PB_SEQ_STREAMS] = {};
     hipEvent_t seq_join[PB_SEQ_STREAMS] = {};
     bool seq_dirty[PB_SEQ_STREAMS] = {};
@@ -454,6 +456,8 @@ static int join_builds(pbgpu_ctx *ctx)
     return PBGPU_OK;
 }
 
+static void slot_counts(const pbgpu_ctx *ctx, const unsigned long long *h, int i, uint64_t *p, uint64_t *b);
+
 #define PB_JOIN(ctx)                         \
     do                                       \
     {                                        \
@@ -577,6 +581,17 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     PB_JOIN(ctx);
     HIPCHK(hipStreamSynchronize(ctx->stream)); // no build still reads the slot's tables
     seq_slot &S = ctx->seqs[seq_idx];
+    if (S.loaded) // the slot's counts so far (their frames follow the old sequence's length)
+    {
+        std::vector<unsigned long long> h(PB_CTR_WORDS);
+        unsigned long long *dc = ctx->d_counters + PB_CTR_WORDS * seq_idx;
+        HIPCHK(hipMemcpy(h.data(), dc, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost));
+        uint64_t p = 0, b = 0;
+        slot_counts(ctx, h.data(), seq_idx, &p, &b);
+        ctx->ctr_base[seq_idx][0] = p;
+        ctx->ctr_base[seq_idx][1] = b;
+        HIPCHK(hipMemset(dc, 0, h.size() * sizeof(h[0])));
+    }
     slot_free(S);
 
     pb_rules_t R = {PB_PAYLOAD_STREAM, PB_FOLD_FULL};
@@ -1776,6 +1791,24 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
     return rc;
 }
 
+// A slot's device counters: the shards' sums; fixed-length kernels add only the bytes they
+// stored (one atomic per workgroup: each is a memory-side transaction, 0.4-1% of a small-frame
+// launch's traffic as two), so their frames are bytes / length.
+static void slot_counts(const pbgpu_ctx *ctx, const unsigned long long *h, int i, uint64_t *p, uint64_t *b)
+{
+    uint64_t pp = 0, bb = 0;
+    for (size_t k = 0; k < PB_CTR_SHARDS; ++k)
+    {
+        pp += h[k * PB_CTR_STRIDE + 0];
+        bb += h[k * PB_CTR_STRIDE + 1];
+    }
+    const seq_slot &S = ctx->seqs[i];
+    if (S.loaded && S.K.fixed_len)
+        pp = bb / S.K.fixed_len;
+    *p = pp + ctx->ctr_base[i][0];
+    *b = bb + ctx->ctr_base[i][1];
+}
+
 int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)
 {
     if (ctx == NULL || n_seq < 0 || n_seq > PB_MAX_SEQUENCES)
@@ -1791,11 +1824,7 @@ int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)
     for (int i = 0; i < n_seq; ++i)
     {
         uint64_t p = 0, b = 0;
-        for (size_t k = 0; k < PB_CTR_SHARDS; ++k)
-        {
-            p += h[PB_CTR_WORDS * i + k * PB_CTR_STRIDE + 0];
-            b += h[PB_CTR_WORDS * i + k * PB_CTR_STRIDE + 1];
-        }
+        slot_counts(ctx, h.data() + PB_CTR_WORDS * i, i, &p, &b);
         if (pckts)
             pckts[i] = p;
         if (bytes)

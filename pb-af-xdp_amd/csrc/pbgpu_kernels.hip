@@ -291,10 +291,13 @@ __device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg)
 // each workgroup adds the frames it built and the bytes it stored (so a skipped store or a
 // short build shows in pbgpu_counters), into shard b % PB_CTR_SHARDS of its sequence — one
 // 128-B line per shard, so neighbouring workgroups' adds do not queue on one address.
+// Fixed-length sequences add only the bytes (one atomic per workgroup; the host takes frames =
+// bytes / length): each device-scope atomic is a memory-side transaction.
 __device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t frames, uint64_t bytes)
 {
     unsigned long long *c = K.counters + (uint64_t)(b % PB_CTR_SHARDS) * PB_CTR_STRIDE;
-    atomicAdd(c, (unsigned long long)frames);
+    if (!K.fixed_len)
+        atomicAdd(c, (unsigned long long)frames);
     atomicAdd(c + 1, (unsigned long long)bytes);
 }
 
