@@ -869,7 +869,8 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 ++K.xs_fp_shift;
             K.xs_np = 256 >> K.xs_fp_shift;
         }
-        else if (minf % 4 == 0 && ((minf <= 64 && 2 * PB_WG / ((4096 + minf - 1) / minf + 1) >= 6) || xp_force) &&
+        else if ((minf % 4 == 0 || (minf % 2 == 0 && xp_force)) &&
+                 ((minf <= 64 && 2 * PB_WG / ((4096 + minf - 1) / minf + 1) >= 6) || xp_force) &&
                  !env_is("PBGPU_KERNEL", "nopage"))
         {
             // pages of frames cut at the page edges (pb_xpage_kernel): one slot per frame

@@ -410,10 +410,11 @@ __device__ __forceinline__ uint32_t pb_swz(uint32_t sl)
 // Frame image d[] -> LDS tile at byte offset B (B has the frame's own alignment
 // mod 16): whole 16-B / 8-B / 4-B words where the frame length allows, byte
 // writes at the two ends of a frame that starts or ends inside a dword.
-template <int NDW>
+// SWZ = false: 16-B / 8-B frames go in unswizzled (a reader that takes the tile in order)
+template <int NDW, bool SWZ = true>
 __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&d)[NDW], uint32_t B, uint32_t flen)
 {
-    if ((flen & 15u) == 0)
+    if (SWZ && (flen & 15u) == 0)
     {
         pb_u32x4 *tile16 = reinterpret_cast<pb_u32x4 *>(s_tile);
         const uint32_t slot0 = B >> 4;
@@ -422,7 +423,7 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
             if ((uint32_t)(4 * t) < flen)
                 tile16[pb_swz(slot0 + (t >> 2))] = pb_u32x4{d[t], d[t + 1], d[t + 2], d[t + 3]};
     }
-    else if ((flen & 7u) == 0)
+    else if (SWZ && (flen & 7u) == 0)
     {
         uint2 *tile8 = reinterpret_cast<uint2 *>(s_tile);
         const uint32_t q0 = B >> 3;
@@ -676,13 +677,18 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
             continue;
         uint32_t d[NDW];
         pb_small_frame<NDW, PROTO, RANDOM>(K, f, d, rtab);
-        const int off = (int)((int64_t)(f * flen) - (int64_t)p0); // (-flen, 4096), dword aligned
+        const int off = (int)((int64_t)(f * flen) - (int64_t)p0); // (-flen, 4096), even
         starts += off >= 0 ? 1u : 0u;
-        uint32_t *row = s_tile + (i * PB_XREG + 128 + off) / 4;
+        if ((flen & 3u) == 0)
+        {
+            uint32_t *row = s_tile + (i * PB_XREG + 128 + off) / 4;
 #pragma unroll
-        for (int t = 0; t < NDW; ++t)
-            if ((uint32_t)(4 * t) < flen)
-                row[t] = d[t];
+            for (int t = 0; t < NDW; ++t)
+                if ((uint32_t)(4 * t) < flen)
+                    row[t] = d[t];
+        }
+        else // 2 mod 4 (98-B ICMP, 106-B UDP): a half dword at one end (pb_small_put)
+            pb_small_put<NDW, false>(s_tile, d, i * PB_XREG + 128 + off, flen);
     }
     // per-wave sums of the frame starts (no init race: one plain write per wave)
     __shared__ uint32_t s_starts[WGT / 64];

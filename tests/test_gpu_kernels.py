@@ -176,7 +176,7 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
         xp_default = flen <= 64 and 512 // ((4096 + flen - 1) // flen + 1) >= 6
         if lin:
             want = "pb_small_kernel<"
-        elif flen % 4 == 0 and (force_xpage or (4096 % flen and xp_default)):
+        elif (flen % 4 == 0 or (force_xpage and flen % 2 == 0)) and (force_xpage or (4096 % flen and xp_default)):
             want = "pb_xpage_kernel"
         else:
             want = "pb_xsmall_kernel" if 4096 % flen == 0 else "pb_small_kernel<"
