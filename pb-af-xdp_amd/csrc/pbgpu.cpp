@@ -863,7 +863,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             K.small_wgt = (w == 64 || w == 128) ? (uint32_t)w : 0u;
         }
         const bool xp_force = env_is("PBGPU_XP_FORCE", "1"); // experiments: pb_xpage_kernel for any length % 4 == 0
-        if (4096 % minf == 0 && !xp_force) // pages of whole frames: pb_xsmall_kernel
+        if (4096 % minf == 0 && minf == 4 * K.small_ndw && !xp_force) // pages of whole frames: pb_xsmall_kernel (64 / 128 B)
         {
             while ((minf << K.xs_fp_shift) < 4096)
                 ++K.xs_fp_shift;

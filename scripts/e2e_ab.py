@@ -42,9 +42,10 @@ for rep in range(int(os.environ.get("REPS", "2"))):
     for tag, extra in variants:
         env = dict(os.environ, PB_SEQ_GAP_MS="0", **extra)
         batch = int(extra.get("GPUBATCH", 1 << 18))
+        nn = int(extra.get("N", n))  # frames of the short run (the long one sends 4x)
         args = extra.get("ARGS", "").split()  # extra command-line arguments ('ARGS=--umemframes 16384')
-        p1, b1, t1 = run(env, lo, hi, n, threads, batch, args)
-        p4, b4, t4 = run(env, lo, hi, 4 * n, threads, batch, args)
+        p1, b1, t1 = run(env, lo, hi, nn, threads, batch, args)
+        p4, b4, t4 = run(env, lo, hi, 4 * nn, threads, batch, args)
         slope = t4 - t1
         print(json.dumps({"case": case, "tag": tag, "env": extra, "threads": threads, "rep": rep,
                           "steady_mpps": round((p4 - p1) / slope / 1e6, 1),
