@@ -2187,9 +2187,6 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
 #ifndef PB_VL_SPLIT
 #define PB_VL_SPLIT 1
 #endif
-#ifndef PB_VL_SYNC
-#define PB_VL_SYNC 0
-#endif
 #ifndef PB_VL_IMGW
 #define PB_VL_IMGW 1 // prologue: header images as NHW dword writes, line map as plain writes + the last line
 #endif
@@ -2469,9 +2466,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
             pb_st16(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
-#if PB_VL_SYNC
-        __syncthreads(); // (A/B) the four waves' stores stay in one 16-KiB step
-#endif
     }
     for (uint32_t s = nfull; s < nsteps; ++s)
     {
