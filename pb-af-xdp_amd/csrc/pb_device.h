@@ -127,6 +127,7 @@ struct pb_kargs
     uint32_t vst;           // 1: the stage_* shape runs pb_vstage_kernel (every payload random, stream rule)
     uint32_t fst_dbg;       // diagnostics (PBGPU_FST_DBG, wrong output): bit 0 skips payload + headers,
                             // bit 1 the stores, bit 3 phase A (time decomposition);
+                            // pb_vline_kernel: bit 0 the stream, bit 2 its arithmetic (constant stores);
                             // pb_vstage_kernel: bit 4 fixed 8-lane groups, bit 5 no 32-lane groups, bit 6 workgroup
                             // edges at frame starts, bit 8 no longest-first window order (A/B)
     uint32_t lds_pad;       // dynamic LDS added to the build launch: caps workgroups per CU (fewer

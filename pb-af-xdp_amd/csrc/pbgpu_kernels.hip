@@ -2422,8 +2422,18 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     // One straight-line path per chunk, and every 128-B line leaves in one store instruction.
     uint8_t *const gout = K.out + wbase + lo_rel;
     const bool store = !(K.fst_dbg & 2u);
-    // (PBGPU_FST_DBG bit 0, diagnostics: the prologue alone, no stream)
-    const uint32_t nsteps = (K.fst_dbg & 1u) ? 0u : (R + PB_VL_STEP - 1u) / PB_VL_STEP;
+    // (PBGPU_FST_DBG diagnostics: bit 0 the prologue alone, no stream; bit 2 the stream's stores
+    // alone, a constant per chunk)
+    const uint32_t nsteps = (K.fst_dbg & 5u) ? 0u : (R + PB_VL_STEP - 1u) / PB_VL_STEP;
+    if (K.fst_dbg & 4u)
+        for (uint32_t s = 0; s < (R + PB_VL_STEP - 1u) / PB_VL_STEP; ++s)
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i)
+            {
+                const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
+                if (c0 < R)
+                    pb_st16(gout + c0, pb_u32x4{c0, s, i, lo_rel});
+            }
     const uint32_t k = lane & 7u, kk = k | (k << 4), ck = (lo_rel >> 4) + k;
     const uint32_t lmax = nlines ? nlines - 1u : 0u;
     // chunk i of step s; clamp: lines past the region's end are computed on its last line
