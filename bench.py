@@ -81,8 +81,16 @@ def init_dist(n_gpus):
         import torch
         import torch.distributed as dist  # noqa: F811
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # PB_DIST_BACKEND=gloo: a rehearsal of the N-rank path on fewer GPUs (ranks share a GPU
+        # round-robin, counters and timings reduce over gloo); the bench itself is RCCL
+        backend = os.environ.get("PB_DIST_BACKEND", "nccl")
+        if backend == "gloo":
+            local %= max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return dist, world, rank, local
 
 

@@ -127,7 +127,9 @@ struct pb_kargs
     uint32_t vst;           // 1: the stage_* shape runs pb_vstage_kernel (every payload random, stream rule)
     uint32_t fst_dbg;       // diagnostics (PBGPU_FST_DBG, wrong output): bit 0 skips payload + headers,
                             // bit 1 the stores, bit 3 phase A (time decomposition);
-                            // pb_vline_kernel: bit 0 the stream, bit 2 its arithmetic (constant stores);
+                            // pb_vline_kernel: bit 0 the stream, bit 2 its arithmetic (constant stores),
+                            // bit 4 the prologue (constant stores over the launch's regions), bit 5
+                            // the payload sums (no orbit-table reads);
                             // pb_vstage_kernel: bit 4 fixed 8-lane groups, bit 5 no 32-lane groups, bit 6 workgroup
                             // edges at frame starts, bit 8 no longest-first window order (A/B)
     uint32_t lds_pad;       // dynamic LDS added to the build launch: caps workgroups per CU (fewer
@@ -153,6 +155,9 @@ struct pb_kargs
     // region's 64-bit start, instead of 8-B offsets; pbgpu.cpp expands them on first use
     uint32_t *offsets32;
     unsigned long long *vl_rstart;
+    // pb_vline_kernel: each frame's L4 payload word sum from pb_vl_psum (null: the prologue
+    // computes it)
+    const uint16_t *vl_psum;
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

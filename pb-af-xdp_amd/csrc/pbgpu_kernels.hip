@@ -163,6 +163,17 @@ __device__ __forceinline__ void pb_st16(uint8_t *p, pb_u32x4 v)
     *reinterpret_cast<pb_u32x4 *>(p) = v;
 #endif
 }
+#ifndef PB_VL_NT
+#define PB_VL_NT 1 // pb_vline_kernel's frame stores are non-temporal
+#endif
+__device__ __forceinline__ void pb_st16_vl(uint8_t *p, pb_u32x4 v)
+{
+#if PB_VL_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
+#else
+    pb_st16(p, v);
+#endif
+}
 
 // 4 payload bytes from 4 consecutive LCG states: byte = state[23:16]
 __device__ __forceinline__ uint32_t pb_pack4(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3)
@@ -2101,6 +2112,9 @@ constexpr uint32_t pb_inv24(uint32_t a)
 constexpr uint32_t PB_A3I = pb_inv24(PB_A3 & PB_M24);
 constexpr uint32_t PB_C3I = (0u - PB_A3I * (PB_C3 & PB_M24)) & PB_M24;
 static_assert(((PB_A3I * (PB_A3 & PB_M24)) & PB_M24) == 1u, "M^-1");
+#ifndef PB_ORB_LOG12
+#define PB_ORB_LOG12 1 // pb_orbit_sum: the discrete log's top 12 bits in closed form (0: 24 steps)
+#endif
 #ifndef PB_ORB_BIDIR
 #define PB_ORB_BIDIR 1 // pb_orbit_sum walks to the nearer prefix-sum sample (<= 16 steps; 0: the next, <= 31)
 #endif
@@ -2113,6 +2127,30 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
 {
     const uint32_t yp = (PB_A3 * st0 + PB_C3) & PB_M24; // the state of payload byte 0
     uint32_t cur = 0, p = 0;
+#if PB_ORB_LOG12
+    // bits 0-11 one at a time; bits 12-23 in closed form: with N = M^4096 = (A, C), A = 1 + 2^14 u,
+    // C = 2^12 v (v odd), N^j(x) = x + j ((A - 1) x + C) mod 2^24 (the dropped terms carry 2^26), so
+    // j = ((yp - cur) >> 12) / (((A - 1) >> 12) yp + v) mod 2^12 (the divisor is odd)
+#pragma unroll
+    for (int i = 0; i < 12; ++i)
+    {
+        const uint32_t bit = 1u << i;
+        const uint32_t nx = __umul24(cur, pb_orb_a(i)) + pb_orb_c(i);
+        const bool take = ((cur ^ yp) & bit) != 0;
+        cur = take ? nx : cur;
+        p |= take ? bit : 0u;
+    }
+    {
+        constexpr uint32_t A12 = pb_orb_a(12), C12 = pb_orb_c(12);
+        static_assert(((A12 - 1u) & 0x3FFFu) == 0u && (C12 & 0x1FFFu) == 0x1000u, "M^4096 shape");
+        const uint32_t w = (__umul24(yp & 0xFFFu, (A12 - 1u) >> 12) + (C12 >> 12)) & 0xFFFu;
+        uint32_t x = w; // w^-1 mod 2^12: correct to 3 bits, each Newton step doubles them
+        x = __umul24(x, (2u - __umul24(w, x)) & 0xFFFu) & 0xFFFu;
+        x = __umul24(x, (2u - __umul24(w, x)) & 0xFFFu) & 0xFFFu;
+        const uint32_t j = __umul24(((yp - cur) >> 12) & 0xFFFu, x) & 0xFFFu;
+        p |= j << 12;
+    }
+#else
 #pragma unroll
     for (int i = 0; i < 24; ++i)
     {
@@ -2122,6 +2160,7 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
         cur = take ? nx : cur;
         p |= take ? bit : 0u;
     }
+#endif
     const uint2 jq = K.jump[n - 1 + PB_JNEG]; // L^(3n): the state one past the payload
     const uint32_t yq = jq.x * yp + jq.y;
     uint32_t q = p + n, wrap = 0;
@@ -2215,6 +2254,38 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     const uint32_t nown = left < WF ? (uint32_t)left : WF;
     const uint64_t fe = f0 + nown;
 
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    if (K.fst_dbg & 16u)
+    {
+        // (PBGPU_FST_DBG bit 4, diagnostics: the stream's stores alone over the launch's own
+        // regions, no prologue — the store shape's time)
+        uint64_t part = 0;
+        for (uint32_t t = tid; t < (bxr & 255u); t += PB_WG)
+            part += K.vblk_sum[(bxr & ~255u) + t];
+#pragma unroll
+        for (uint32_t dd = 32; dd > 0; dd >>= 1)
+            part += __shfl_xor(part, dd, 64);
+        if (lane == 0u)
+            reinterpret_cast<uint64_t *>(s_dyn)[wv] = part;
+        __syncthreads();
+        uint64_t S = K.vblk_l2[bxr >> 8];
+#pragma unroll
+        for (uint32_t w = 0; w < PB_WG / 64; ++w)
+            S += reinterpret_cast<uint64_t *>(s_dyn)[w];
+        const uint64_t lo = bxr ? (S & ~127ull) : 0ull;
+        const uint64_t hi = bxr + 1u < gridDim.x ? ((S + K.vblk_sum[bxr]) & ~127ull) : lo;
+        const uint32_t R = (uint32_t)(hi - lo);
+        for (uint32_t s = 0; s < (R + PB_VL_STEP - 1u) / PB_VL_STEP; ++s)
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i)
+            {
+                const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
+                if (c0 < R)
+                    pb_st16_vl(K.out + lo + c0, pb_u32x4{c0, s, i, (uint32_t)lo});
+            }
+        return;
+    }
+
     // ---------------- prologue: one lane per frame slot ----------------
     const int64_t fb = (int64_t)f0 - (int64_t)GH;
     uint64_t s0_part = 0;
@@ -2253,7 +2324,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
                           pb_halves(d[13]);
             if (flags & PBK_PSEUDO)
                 hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
-            const uint32_t c = (~pb_fold(pb_fold(hs) + pb_orbit_sum(K, P.st0, P.plen))) & 0xFFFFu;
+            // (PBGPU_FST_DBG bit 5, diagnostics: no payload sum, the orbit-table reads skipped)
+            const uint32_t ps = (K.fst_dbg & 32u) ? 0u : (K.vl_psum ? (uint32_t)K.vl_psum[fj] : pb_orbit_sum(K, P.st0, P.plen));
+            const uint32_t c = (~pb_fold(pb_fold(hs) + ps)) & 0xFFFFu;
             const uint32_t cv = K.csum_hi ? (c << 16) : c;
 #pragma unroll
             for (uint32_t w = 0; w < 16; ++w)
@@ -2261,7 +2334,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         }
     }
     // frame starts: exclusive scan of the slot lengths (in-wave shuffles, wave totals via LDS)
-    const uint32_t lane = tid & 63u, wv = tid >> 6;
     uint32_t inc = flen;
 #pragma unroll
     for (uint32_t dd = 1; dd < 64; dd <<= 1)
@@ -2432,7 +2504,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             {
                 const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
                 if (c0 < R)
-                    pb_st16(gout + c0, pb_u32x4{c0, s, i, lo_rel});
+                    pb_st16_vl(gout + c0, pb_u32x4{c0, s, i, lo_rel});
             }
     const uint32_t k = lane & 7u, kk = k | (k << 4), ck = (lo_rel >> 4) + k;
     const uint32_t lmax = nlines ? nlines - 1u : 0u;
@@ -2475,7 +2547,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             v[i] = chunk(s, i, false);
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
-            pb_st16(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
+            pb_st16_vl(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
     }
     for (uint32_t s = nfull; s < nsteps; ++s)
     {
@@ -2489,7 +2561,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         {
             const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
             if (store && c0 < R)
-                pb_st16(gout + c0, v[i]);
+                pb_st16_vl(gout + c0, v[i]);
         }
     }
     if (tid == 0) // the workgroup stores exactly [lo, hi) (the launch's last chunk zero-padded)
@@ -2913,6 +2985,28 @@ __global__ __launch_bounds__(256) void pb_len_wgsum(pb_kargs K, uint32_t wgf, ui
     __syncthreads();
     if (threadIdx.x == 0)
         l2[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// pb_vline_kernel's payload sums ahead of the build: lane f the L4 payload word sum of frame f
+// (pb_orbit_sum), so the orbit-table reads run while no frame stream evicts the table from L2
+__global__ __launch_bounds__(256) void pb_vl_psum(pb_kargs K, uint16_t *psum)
+{
+    const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (f >= K.n_frames)
+        return;
+    uint64_t k;
+    uint32_t pi;
+    pb_frame_index(K, f, k, pi);
+    const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+    const pb_frame_pl P = pb_payload<false>(K, s, pi);
+    psum[f] = (uint16_t)pb_orbit_sum(K, P.st0, P.plen);
+}
+
+extern "C" hipError_t pbk_launch_vl_psum(const pb_kargs *K, uint16_t *psum, hipStream_t st)
+{
+    const uint32_t grid = (uint32_t)((K->n_frames + 255) / 256);
+    hipLaunchKernelGGL(pb_vl_psum, dim3(grid), dim3(256), 0, st, *K, psum);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t wgf, uint32_t *bsum, uint32_t nblk,

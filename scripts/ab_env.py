@@ -16,6 +16,8 @@ for v in sys.argv[3:]:
     variants.append((tag, dict(e.split("=", 1) for e in envs.split(",") if e)))
 keys = {k for _, e in variants for k in e}
 ctx = GpuContext(0)
+if os.environ.get("SPAN"):  # one event pair around all of a rep's builds: pre-passes included
+    ctx.set_timing(ctx.TIMING_SPAN)
 seq = Sequence.from_config(pc.get(cfg))
 res = {t: [] for t, _ in variants}
 # clock ramp: ~0.5 s of untimed launches (bench.py run_config)

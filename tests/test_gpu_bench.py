@@ -92,6 +92,25 @@ def test_bench_mix_under_torchrun_reduces_counters():
     assert len(d["roofline"]["kernel"]) == 3
 
 
+def test_bench_two_ranks_share_the_gpu_over_gloo():
+    """The N-rank path with real builds: two ranks on one GPU (PB_DIST_BACKEND=gloo), each
+    building its own shard of every step; the reduced counters cover both ranks' frames."""
+    n, steps, world = 1 << 19, 3, 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus",
+           str(world), "--steps", str(steps), "--warmup", "1", "--packets", str(n), "--ramp-seconds", "0.05",
+           "--cpu-seconds", "0", "--config", "c5_mix"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PB_DIST_BACKEND="gloo")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = _line(out)
+    assert d["n_gpus"] == world
+    gc = d["global_counters"]
+    assert gc["packets"] == [n * steps * world] * 3
+    assert gc["bytes"] == [n * steps * world * 64, n * steps * world * 60, n * steps * world * 98]
+    assert abs(d["value"] - world * 3 * n / (d["ms_per_step"] * 1e-3) / 1e6) < 0.01 * d["value"]
+
+
 def test_bench_tcp_syn_line():
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--packets",
            str(1 << 20), "--ramp-seconds", "0.05", "--cpu-seconds", "0", "--config", "c4_tcp_syn"]
