@@ -155,9 +155,6 @@ struct pb_kargs
     // region's 64-bit start, instead of 8-B offsets; pbgpu.cpp expands them on first use
     uint32_t *offsets32;
     unsigned long long *vl_rstart;
-    // pb_vline_kernel: each frame's L4 payload word sum from pb_vl_psum (null: the prologue
-    // computes it)
-    const uint16_t *vl_psum;
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

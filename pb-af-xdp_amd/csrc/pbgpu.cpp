@@ -26,7 +26,6 @@
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st);
 extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
                                          uint64_t *offsets, hipStream_t st);
-extern "C" hipError_t pbk_launch_vl_psum(const pb_kargs *K, uint16_t *psum, hipStream_t st);
 extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t wgf, uint32_t *bsum, uint32_t nblk,
                                              unsigned long long *l2, uint32_t n_l2, uint64_t *offsets, hipStream_t st);
 extern "C" hipError_t pbk_launch_expand_offsets(const uint32_t *off32, const unsigned long long *rstart, uint32_t wf,
@@ -127,7 +126,6 @@ struct frames_events
     // on first use (packed32 set until then)
     uint32_t *d_off32 = nullptr;
     unsigned long long *d_rstart = nullptr;
-    uint16_t *d_psum = nullptr; // pb_vl_psum's per-frame payload sums
     bool packed32 = false;
     uint32_t wf = 0;
 };
@@ -1203,8 +1201,6 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
             (void)hipEventDestroy(fe->moved);
         if (fe->d_off32)
             (void)hipFree(fe->d_off32);
-        if (fe->d_psum)
-            (void)hipFree(fe->d_psum);
         if (fe->d_rstart)
             (void)hipFree(fe->d_rstart);
         if (fe->landed)
@@ -1404,14 +1400,6 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
                 }
                 K.offsets32 = fe->d_off32;
                 K.vl_rstart = fe->d_rstart;
-                K.vl_psum = nullptr;
-                if ((K.flags & PBK_L4_CSUM) && env_int("PBGPU_VL_PSUM", 0))
-                {
-                    if (fe->d_psum == nullptr)
-                        HIPCHK(hipMalloc((void **)&fe->d_psum, (out->capacity_frames + 1) * sizeof(uint16_t)));
-                    HIPCHK(pbk_launch_vl_psum(&K, fe->d_psum, st));
-                    K.vl_psum = fe->d_psum;
-                }
                 fe->packed32 = true;
                 fe->wf = wgf;
             }

@@ -2325,7 +2325,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             if (flags & PBK_PSEUDO)
                 hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
             // (PBGPU_FST_DBG bit 5, diagnostics: no payload sum, the orbit-table reads skipped)
-            const uint32_t ps = (K.fst_dbg & 32u) ? 0u : (K.vl_psum ? (uint32_t)K.vl_psum[fj] : pb_orbit_sum(K, P.st0, P.plen));
+            const uint32_t ps = (K.fst_dbg & 32u) ? 0u : pb_orbit_sum(K, P.st0, P.plen);
             const uint32_t c = (~pb_fold(pb_fold(hs) + ps)) & 0xFFFFu;
             const uint32_t cv = K.csum_hi ? (c << 16) : c;
 #pragma unroll
@@ -2985,28 +2985,6 @@ __global__ __launch_bounds__(256) void pb_len_wgsum(pb_kargs K, uint32_t wgf, ui
     __syncthreads();
     if (threadIdx.x == 0)
         l2[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-}
-
-// pb_vline_kernel's payload sums ahead of the build: lane f the L4 payload word sum of frame f
-// (pb_orbit_sum), so the orbit-table reads run while no frame stream evicts the table from L2
-__global__ __launch_bounds__(256) void pb_vl_psum(pb_kargs K, uint16_t *psum)
-{
-    const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (f >= K.n_frames)
-        return;
-    uint64_t k;
-    uint32_t pi;
-    pb_frame_index(K, f, k, pi);
-    const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
-    const pb_frame_pl P = pb_payload<false>(K, s, pi);
-    psum[f] = (uint16_t)pb_orbit_sum(K, P.st0, P.plen);
-}
-
-extern "C" hipError_t pbk_launch_vl_psum(const pb_kargs *K, uint16_t *psum, hipStream_t st)
-{
-    const uint32_t grid = (uint32_t)((K->n_frames + 255) / 256);
-    hipLaunchKernelGGL(pb_vl_psum, dim3(grid), dim3(256), 0, st, *K, psum);
-    return hipGetLastError();
 }
 
 extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t wgf, uint32_t *bsum, uint32_t nblk,

@@ -20,6 +20,9 @@ for v in sys.argv[3:]:
 keys = {k for _, _, e in variants for k in e}
 seq = Sequence.from_config(pc.get(cfg))
 ctxs = {t: GpuContext(0, lib_path=p) for t, p, _ in variants}
+if os.environ.get("SPAN"):  # one event pair around all of a rep's builds (no per-launch L2 write-back)
+    for c in ctxs.values():
+        c.set_timing(c.TIMING_SPAN)
 res = {t: [] for t, _, _ in variants}
 names = {}
 

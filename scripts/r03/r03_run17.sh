@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 3: pb_vline_kernel's prologue cost in context: full / without the payload sums' orbit
 # reads (PBGPU_FST_DBG bit 5), prologue + constant stores with and without them (bit 2), the
-# payload sums in a pass of their own ahead of the build (PBGPU_VL_PSUM=1, and its parity), the
+# payload sums in a pass of their own ahead of the build (PBGPU_VL_PSUM=1, a build of round 3 that was
+# measured and removed, and its parity), the
 # stores alone (bit 4).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=${OUT:-gpurun_out/r03s2q}
