@@ -163,6 +163,28 @@ __device__ __forceinline__ void pb_st16(uint8_t *p, pb_u32x4 v)
     *reinterpret_cast<pb_u32x4 *>(p) = v;
 #endif
 }
+#ifndef PB_SX_NT
+#define PB_SX_NT 1 // pb_small_kernel's and pb_xpage_kernel's stores are non-temporal
+#endif
+#ifndef PB_XS_NT
+#define PB_XS_NT 0 // (A/B builds) pb_xsmall_kernel's stores non-temporal
+#endif
+__device__ __forceinline__ void pb_st16_xs(uint8_t *p, pb_u32x4 v)
+{
+#if PB_XS_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
+#else
+    pb_st16(p, v);
+#endif
+}
+__device__ __forceinline__ void pb_st16_sx(uint8_t *p, pb_u32x4 v)
+{
+#if PB_SX_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
+#else
+    pb_st16(p, v);
+#endif
+}
 #ifndef PB_VL_NT
 #define PB_VL_NT 1 // pb_vline_kernel's frame stores are non-temporal
 #endif
@@ -545,7 +567,7 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
             for (int t = 0; t < 4; ++t)
                 v[t] &= pb_range_mask(0, (int)tile_bytes - (int)(16 * c + 4 * t));
         }
-        pb_st16(out + 16 * c, v);
+        pb_st16_sx(out + 16 * c, v);
     }
     if (tid == 0)
         pb_count(K, blockIdx.x, nfr, tile_bytes);
@@ -613,7 +635,7 @@ __global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
                 for (int t = 0; t < 4; ++t)
                     v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
             }
-            pb_st16(K.out + o, v);
+            pb_st16_xs(K.out + o, v);
         }
     }
     if (tid == 0)
@@ -725,7 +747,7 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
                 for (int t = 0; t < 4; ++t)
                     v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
             }
-            pb_st16(K.out + o, v);
+            pb_st16_sx(K.out + o, v);
         }
     }
     if (tid == 0)
