@@ -166,6 +166,17 @@ __device__ __forceinline__ void pb_st16(uint8_t *p, pb_u32x4 v)
 #ifndef PB_SX_NT
 #define PB_SX_NT 1 // pb_small_kernel's and pb_xpage_kernel's stores are non-temporal
 #endif
+#ifndef PB_FS_NT
+#define PB_FS_NT 0 // (A/B builds) pb_fstage_kernel's stores non-temporal
+#endif
+__device__ __forceinline__ void pb_st16_fs(uint8_t *p, pb_u32x4 v)
+{
+#if PB_FS_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
+#else
+    pb_st16(p, v);
+#endif
+}
 #ifndef PB_XS_NT
 #define PB_XS_NT 0 // (A/B builds) pb_xsmall_kernel's stores non-temporal
 #endif
@@ -1561,13 +1572,13 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
         for (; c + 3 * PB_WG < c1; c += 4 * PB_WG)
         {
             const pb_u32x4 v0 = st16[c], v1 = st16[c + PB_WG], v2 = st16[c + 2 * PB_WG], v3 = st16[c + 3 * PB_WG];
-            pb_st16(gout + 16 * c, v0);
-            pb_st16(gout + 16 * (c + PB_WG), v1);
-            pb_st16(gout + 16 * (c + 2 * PB_WG), v2);
-            pb_st16(gout + 16 * (c + 3 * PB_WG), v3);
+            pb_st16_fs(gout + 16 * c, v0);
+            pb_st16_fs(gout + 16 * (c + PB_WG), v1);
+            pb_st16_fs(gout + 16 * (c + 2 * PB_WG), v2);
+            pb_st16_fs(gout + 16 * (c + 3 * PB_WG), v3);
         }
         for (; c < c1; c += PB_WG)
-            pb_st16(gout + 16 * c, st16[c]);
+            pb_st16_fs(gout + 16 * c, st16[c]);
         if (tid == PB_WG - 1 && (R1 & 15u))
         {
             const uint32_t *sw = reinterpret_cast<const uint32_t *>(stg) + 4 * c1;
