@@ -163,6 +163,9 @@ __device__ __forceinline__ void pb_st16(uint8_t *p, pb_u32x4 v)
     *reinterpret_cast<pb_u32x4 *>(p) = v;
 #endif
 }
+#ifndef PB_SMALL_DYN
+#define PB_SMALL_DYN 0 // pb_small_kernel's LDS tile sized to its frames (dynamic) instead of WGT * NDW dwords
+#endif
 #ifndef PB_SX_NT
 #define PB_SX_NT 1 // pb_small_kernel's and pb_xpage_kernel's stores are non-temporal
 #endif
@@ -549,7 +552,11 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
 template <int NDW, int PROTO, bool RANDOM, int WGT>
 __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
 {
+#if PB_SMALL_DYN
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[]; // pb_small_tile_bytes(WGT, flen)
+#else
     __shared__ __attribute__((aligned(16))) uint32_t s_tile[WGT * NDW + 8];
+#endif
     const uint32_t tid = threadIdx.x;
     const uint64_t f0 = (uint64_t)(PB_SMALL_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x) : blockIdx.x) * WGT;
     const uint64_t left = K.n_frames - f0;
@@ -2781,6 +2788,13 @@ __global__ __launch_bounds__(256) void pb_fillreg_kernel(pb_u32x4 *dst, uint64_t
 
 // ---------------- launch wrappers (called from pbgpu.cpp) ----------------
 
+// pb_small_kernel's LDS tile: the workgroup's frames, not WGT slots of 4 * NDW bytes (98-B frames:
+// 6.2 instead of 8.2 KiB, 26 instead of 19 workgroups per CU)
+static size_t pb_small_tile_bytes(uint32_t wgt, uint32_t flen)
+{
+    return PB_SMALL_DYN ? (((size_t)wgt * flen + 15) & ~(size_t)15) + 32 : 0;
+}
+
 template <int NDW, int PROTO>
 static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
 {
@@ -2806,11 +2820,11 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
             const uint32_t wgt = K->small_wgt ? K->small_wgt : PB_WG;
             const uint32_t g = (uint32_t)((K->n_frames + wgt - 1) / wgt);
             if (wgt == 64)
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, 64>), dim3(g), dim3(64), K->lds_pad, st, *K);
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, 64>), dim3(g), dim3(64), pb_small_tile_bytes(64, K->fixed_len) + K->lds_pad, st, *K);
             else if (wgt == 128)
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, 128>), dim3(g), dim3(128), K->lds_pad, st, *K);
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, 128>), dim3(g), dim3(128), pb_small_tile_bytes(128, K->fixed_len) + K->lds_pad, st, *K);
             else
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, PB_WG>), dim3(g), dim3(PB_WG), K->lds_pad, st, *K);
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, PB_WG>), dim3(g), dim3(PB_WG), pb_small_tile_bytes(PB_WG, K->fixed_len) + K->lds_pad, st, *K);
         }
     }
     else
@@ -2822,11 +2836,11 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
             const uint32_t wgt = K->small_wgt ? K->small_wgt : PB_WG;
             const uint32_t g = (uint32_t)((K->n_frames + wgt - 1) / wgt);
             if (wgt == 64)
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, 64>), dim3(g), dim3(64), K->lds_pad, st, *K);
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, 64>), dim3(g), dim3(64), pb_small_tile_bytes(64, K->fixed_len) + K->lds_pad, st, *K);
             else if (wgt == 128)
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, 128>), dim3(g), dim3(128), K->lds_pad, st, *K);
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, 128>), dim3(g), dim3(128), pb_small_tile_bytes(128, K->fixed_len) + K->lds_pad, st, *K);
             else
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, PB_WG>), dim3(g), dim3(PB_WG), K->lds_pad, st, *K);
+                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, PB_WG>), dim3(g), dim3(PB_WG), pb_small_tile_bytes(PB_WG, K->fixed_len) + K->lds_pad, st, *K);
         }
     }
 }
