@@ -14,3 +14,8 @@ SPAN=1 REPS=12 timeout -k 10 300 python -u scripts/ab_lib.py c5_icmp_echo 335544
 cat $O/ab_c5_icmp_echo_dyn.jsonl
 timeout -k 10 200 python3 bench.py --steps 50 --warmup 5 --no-variants --cpu-seconds 0 --config c5_mix > $O/c5_mix.json || exit 1
 python3 -c "import json; d=json.load(open('$O/c5_mix.json')); print('c5_mix', d['ms_per_step'], d['roofline']['frac'])"
+# orbit samples every 16th / 8th position (PB_ORB_SH=4 / 3: 4 / 8-MiB tables, walks <= 8 / 4) now
+# that the frame stores are non-temporal, against every 32nd (the library)
+SPAN=1 REPS=8 timeout -k 10 500 python -u scripts/ab_lib.py c3_udp_var 33554432 sh5:/tmp/libpbgpu_static.so \
+    sh4:$V/libpbgpu_sh4.so sh3:$V/libpbgpu_sh3.so > $O/ab_c3_orbsh_nt.jsonl 2>&1 || exit 1
+cat $O/ab_c3_orbsh_nt.jsonl
