@@ -164,7 +164,7 @@ __device__ __forceinline__ void pb_st16(uint8_t *p, pb_u32x4 v)
 #endif
 }
 #ifndef PB_SMALL_DYN
-#define PB_SMALL_DYN 0 // pb_small_kernel's LDS tile sized to its frames (dynamic) instead of WGT * NDW dwords
+#define PB_SMALL_DYN 1 // pb_small_kernel's LDS tile sized to its frames (dynamic) instead of WGT * NDW dwords
 #endif
 #ifndef PB_SX_NT
 #define PB_SX_NT 1 // pb_small_kernel's and pb_xpage_kernel's stores are non-temporal
