@@ -70,11 +70,21 @@ uint32_t pbo_seed(uint64_t seed_base, uint16_t seq_idx, uint64_t k)
     return (uint32_t)splitmix64(seed_base ^ (((uint64_t)seq_idx << 48) + k));
 }
 
-/* PB-Common rand_num(min, max, seed) — expected form (UNPINNED): the seed is
- * taken by value, so every call in one iteration sees the same first draw. */
+/* PB-Common rand_num(min, max, seed): min + rand_r(&copy) % (max - min + 1).
+ * The seed is taken by value, so every call in one iteration sees the same
+ * first draw.  PINNED by the reference's own captures: images/test1.gif's
+ * five and images/test2.gif's eight consecutive-second source ports (README.md
+ * :23-27; the demo build seeded with time(NULL)) are 1 + rand_r(t) % 65535 at
+ * consecutive t, and no other modulus / offset reproduces them
+ * (tests/golden/kat_gif_ports.json, tests/test_rand_num_pin.py). */
 static int rand_num(int min, int max, unsigned int seed)
 {
     return (pbo_rand_r(&seed) % (max - min + 1)) + min;
+}
+
+int pbo_rand_num(int min, int max, unsigned int seed)
+{
+    return rand_num(min, max, seed);
 }
 
 /* --------------------------------------------------------- checksums -- */

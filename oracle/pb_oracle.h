@@ -9,8 +9,12 @@
  *   pinned  : glibc rand_r (tests compare against the host libc); the UDP
  *             checksum composition and the IPv4 header checksum (the two
  *             known-answer frames of images/test1.gif, README.md:23 —
- *             transcribed in SURVEY.md Appendix C, fixtures under tests/golden).
- *   UNPINNED: rand_num's modulo form, rand_ip's host-bit rule, the TCP/ICMP
+ *             transcribed in SURVEY.md Appendix C, fixtures under tests/golden);
+ *             rand_num's form min + rand_r % (max - min + 1), which sets TTL,
+ *             ID, range index, ports and payload length (the consecutive-second
+ *             source ports of images/test1.gif and test2.gif,
+ *             tests/golden/kat_gif_ports.json).
+ *   UNPINNED: rand_ip's host-bit rule, the TCP/ICMP
  *             checksum composition, the IPv4 single- vs full-fold edge case,
  *             UDP 0-checksum mapping.  These live in the un-vendored PB-Common
  *             submodule (modules/common is empty in /root/reference); the
@@ -28,6 +32,8 @@ extern "C" {
 
 /* glibc rand_r restated (3-step LCG, 31-bit output). */
 int pbo_rand_r(unsigned int *seed);
+/* PB-Common rand_num(min, max, seed) with the seed by value (pinned, see .c). */
+int pbo_rand_num(int min, int max, unsigned int seed);
 
 /* Per-iteration seed stream (pb_config.h). */
 uint32_t pbo_seed(uint64_t seed_base, uint16_t seq_idx, uint64_t k);

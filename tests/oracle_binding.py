@@ -28,6 +28,8 @@ def lib():
         L = C.CDLL(ORACLE_LIB)
         L.pbo_rand_r.restype = C.c_int
         L.pbo_rand_r.argtypes = [C.POINTER(C.c_uint)]
+        L.pbo_rand_num.restype = C.c_int
+        L.pbo_rand_num.argtypes = [C.c_int, C.c_int, C.c_uint]
         L.pbo_seed.restype = C.c_uint32
         L.pbo_seed.argtypes = [C.c_uint64, C.c_uint16, C.c_uint64]
         L.pbo_build.restype = C.c_int
@@ -52,6 +54,10 @@ def rand_r(seed: int):
     s = C.c_uint(seed)
     r = lib().pbo_rand_r(C.byref(s))
     return r, s.value
+
+
+def rand_num(lo: int, hi: int, seed: int) -> int:
+    return lib().pbo_rand_num(lo, hi, seed)
 
 
 def seed(seed_base: int, seq_idx: int, k: int) -> int:
