@@ -23,7 +23,9 @@
 #define PB_XREG (PB_XPG + 256)             // LDS bytes per page region (128 B slack either side)
 #define PBK_FILL_SHAPES 15                 // write-roofline probe shapes (pbk_launch_fill)
 #define PB_XNP_MAX 8                       // pb_xsmall_kernel: pages per workgroup, 4 (64-B frames) or 8 (128-B)
+#ifndef PB_CTR_SHARDS
 #define PB_CTR_SHARDS 64                   // per-sequence counter shards (workgroup b adds to shard b % 64)
+#endif
 #define PB_CTR_STRIDE 16                   // u64 words per shard: one 128-B line each ({frames, bytes} + pad)
 
 // glibc LCG
@@ -129,7 +131,8 @@ struct pb_kargs
                             // bit 1 the stores, bit 3 phase A (time decomposition);
                             // pb_vline_kernel: bit 0 the stream, bit 2 its arithmetic (constant stores),
                             // bit 4 the prologue (constant stores over the launch's regions), bit 5
-                            // the payload sums (no orbit-table reads);
+                            // the payload sums (no orbit-table reads), bit 6 the orbit-table reads
+                            // alone (sums computed from the entries' indices);
                             // pb_vstage_kernel: bit 4 fixed 8-lane groups, bit 5 no 32-lane groups, bit 6 workgroup
                             // edges at frame starts, bit 8 no longest-first window order (A/B)
     uint32_t lds_pad;       // dynamic LDS added to the build launch: caps workgroups per CU (fewer
@@ -155,6 +158,9 @@ struct pb_kargs
     // region's 64-bit start, instead of 8-B offsets; pbgpu.cpp expands them on first use
     uint32_t *offsets32;
     unsigned long long *vl_rstart;
+    // pb_xpage_kernel: 1 when the launch's last page index times 4096 % flen reaches 2^31 (the
+    // first frame of a page then takes the 64-bit path)
+    uint32_t xp_fa_hi;
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

@@ -11,11 +11,14 @@
 #include <ctype.h>
 #include <stddef.h>
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <new>
 #include <deque>
 #include <vector>
@@ -1070,8 +1073,11 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 }
                 if (ctx->d_orbit == nullptr)
                 {
-                    uint32_t tot = 0;
-                    std::vector<uint32_t> orb = make_orbit_table(&tot);
+                    // the 2^24-step walk runs once per process; each context uploads the result
+                    static std::once_flag once;
+                    static std::vector<uint32_t> orb;
+                    static uint32_t tot = 0;
+                    std::call_once(once, [] { orb = make_orbit_table(&tot); });
                     int rc2 = upload(&ctx->d_orbit, orb.data(), orb.size());
                     if (rc2 != PBGPU_OK)
                         return rc2;
@@ -1393,11 +1399,12 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             if (K.vl)
             {
                 // 4 B per frame and 8 B per region instead of 8 B per frame
+                // (each checked on its own: a failed second allocation must not leave the pair
+                // half set for the next build to launch with a null region-start array)
                 if (fe->d_off32 == nullptr)
-                {
                     HIPCHK(hipMalloc((void **)&fe->d_off32, (out->capacity_frames + 1) * sizeof(uint32_t)));
+                if (fe->d_rstart == nullptr)
                     HIPCHK(hipMalloc((void **)&fe->d_rstart, (out->capacity_frames / 32 + 2) * sizeof(unsigned long long)));
-                }
                 K.offsets32 = fe->d_off32;
                 K.vl_rstart = fe->d_rstart;
                 fe->packed32 = true;
@@ -1421,6 +1428,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             const uint32_t np = K.xs_np;
             K.xs_full = (uint32_t)(nch / (8 * np) * 8);
             K.xs_grid = K.xs_full + (uint32_t)((nch - (uint64_t)K.xs_full * np + np - 1) / np);
+            K.xp_fa_hi = K.xp && (uint64_t)nch * (4096 % K.fixed_len) >= (1ull << 31);
         }
     }
     timing_pair tp = {nullptr, nullptr};
@@ -1599,6 +1607,32 @@ static uint8_t *mapped(pbgpu_ctx *ctx, uint8_t *p, uint64_t n)
     return NULL;
 }
 
+// Wait for a landing's event without paying a blocking wait's wake-up latency on short waits,
+// and without holding a core for long ones (each TX thread waits this way; the GPU box gives a
+// process a 16-CPU quota): poll for up to 50 us, then poll with sched_yield() between queries
+// for up to 2 ms, then block in the runtime.
+static double now_s()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static hipError_t spin_wait(hipEvent_t ev)
+{
+    hipError_t e;
+    const double t0 = now_s();
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady)
+    {
+        const double dt = now_s() - t0;
+        if (dt > 2e-3)
+            return hipEventSynchronize(ev);
+        if (dt > 50e-6)
+            sched_yield();
+    }
+    return e;
+}
+
 int pbgpu_land_wait(pbgpu_ctx *ctx, uint32_t keep)
 {
     if (ctx == NULL)
@@ -1610,8 +1644,7 @@ int pbgpu_land_wait(pbgpu_ctx *ctx, uint32_t keep)
         // (a blocking wait adds its wake-up latency to each landing; PBGPU_LAND_SPIN=0 blocks)
         hipError_t e = hipSuccess;
         if (ctx->land_spin)
-            while ((e = hipEventQuery(op.ev)) == hipErrorNotReady)
-                ;
+            e = spin_wait(op.ev);
         else
             e = hipEventSynchronize(op.ev);
         ctx->landings.pop_front();
@@ -1979,12 +2012,14 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
+    else if (K.xs_np && K.xp && !env_is("PBGPU_KERNEL", "linear"))
+        snprintf(buf, n, "pb_xpage_kernel<%u, %u, %s, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
+                 K.xp_wgt, K.fixed_len % 4 == 0 ? "true" : "false");
     else if (K.xs_np && !env_is("PBGPU_KERNEL", "linear"))
-        snprintf(buf, n, "%s<%u, %u, %s>", K.xp ? "pb_xpage_kernel" : "pb_xsmall_kernel", K.small_ndw, K.proto,
-                 K.pl0.random ? "true" : "false");
+        snprintf(buf, n, "pb_xsmall_kernel<%u, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
     else
-        snprintf(buf, n, "pb_small_kernel<%u, %u, %s, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
-                 K.small_wgt ? K.small_wgt : (uint32_t)PB_WG);
+        snprintf(buf, n, "pb_small_kernel<%u, %u, %s, %u, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
+                 K.small_wgt ? K.small_wgt : (uint32_t)PB_WG, K.fixed_len % 4 == 2 ? 2u : 0u);
     return PBGPU_OK;
 }
 

@@ -340,8 +340,13 @@ __device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg)
 // 128-B line per shard, so neighbouring workgroups' adds do not queue on one address.
 // Fixed-length sequences add only the bytes (one atomic per workgroup; the host takes frames =
 // bytes / length): each device-scope atomic is a memory-side transaction.
+#ifndef PB_COUNT
+#define PB_COUNT 1 // (A/B builds) 0: no counter atomics (wrong counters; measures their cost)
+#endif
 __device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t frames, uint64_t bytes)
 {
+    if (!PB_COUNT)
+        return;
     unsigned long long *c = K.counters + (uint64_t)(b % PB_CTR_SHARDS) * PB_CTR_STRIDE;
     if (!K.fixed_len)
         atomicAdd(c, (unsigned long long)frames);
@@ -457,10 +462,21 @@ __device__ __forceinline__ uint32_t pb_swz(uint32_t sl)
 // Frame image d[] -> LDS tile at byte offset B (B has the frame's own alignment
 // mod 16): whole 16-B / 8-B / 4-B words where the frame length allows, byte
 // writes at the two ends of a frame that starts or ends inside a dword.
+// two dwords at a 4-B aligned LDS address: one ds_write2_b32
+typedef uint32_t pb_u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+
 // SWZ = false: 16-B / 8-B frames go in unswizzled (a reader that takes the tile in order)
-template <int NDW, bool SWZ = true>
+// AL: the frame length's alignment class when the kernel knows it (16: flen % 16 == 0, 4: % 4,
+// 2: 2 mod 4; 0: any, chosen at run time) - the other paths are not compiled in
+template <int NDW, bool SWZ = true, int AL = 0>
 __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&d)[NDW], uint32_t B, uint32_t flen)
 {
+    if (AL == 16)
+        __builtin_assume((flen & 15u) == 0);
+    else if (AL == 4)
+        __builtin_assume((flen & 3u) == 0);
+    else if (AL == 2)
+        __builtin_assume((flen & 3u) == 2u);
     if (SWZ && (flen & 15u) == 0)
     {
         pb_u32x4 *tile16 = reinterpret_cast<pb_u32x4 *>(s_tile);
@@ -511,8 +527,7 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
                 if ((uint32_t)u + 1u < nw)
                 {
                     const uint32_t v1 = __builtin_amdgcn_alignbyte(u + 2 < NDW ? d[u + 2] : 0u, d[u + 1], sh);
-                    const uint2 pr = make_uint2(v0, v1);
-                    __builtin_memcpy(row + u, &pr, 8);
+                    *reinterpret_cast<pb_u32x2a4 *>(row + u) = pb_u32x2a4{v0, v1};
                 }
                 else
                     row[u] = v0;
@@ -549,7 +564,7 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
 // Linear form: workgroup b builds frames [WGT b, WGT b + WGT) and writes their
 // contiguous byte range (WGT = 256, or 128 / 64: smaller regions per workgroup).  Used when the output is not 4 KiB aligned (and under
 // PBGPU_KERNEL=linear for comparison).
-template <int NDW, int PROTO, bool RANDOM, int WGT>
+template <int NDW, int PROTO, bool RANDOM, int WGT, int AL = 0> // AL: pb_small_put's alignment class
 __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
 {
 #if PB_SMALL_DYN
@@ -567,7 +582,7 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
     {
         uint32_t d[NDW];
         pb_small_frame<NDW, PROTO, RANDOM>(K, f0 + tid, d);
-        pb_small_put<NDW>(s_tile, d, tid * flen, flen);
+        pb_small_put<NDW, true, AL>(s_tile, d, tid * flen, flen);
     }
     __syncthreads();
 
@@ -632,7 +647,7 @@ __global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
         {
             uint32_t d[NDW];
             pb_small_frame<NDW, PROTO, RANDOM>(K, f, d);
-            pb_small_put<NDW>(s_tile, d, i * PB_XREG + 128 + j * flen, flen);
+            pb_small_put<NDW, true, 16>(s_tile, d, i * PB_XREG + 128 + j * flen, flen); // flen = 64 / 128 B
         }
     }
     __syncthreads();
@@ -666,7 +681,7 @@ __global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
             if (c < K.xs_nch)
                 by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
         }
-        pb_count(K, b, by >> (12u - K.xs_fp_shift), by);
+        pb_count(K, b, 0, by); // fixed length: frames = bytes / length on the host
     }
 }
 
@@ -678,7 +693,27 @@ __global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
 // whole into the page's LDS region, whose 128 B of slack either side take the
 // bytes outside the page and are never stored.  At 60 B one frame in 69 is built
 // twice.
-template <int NDW, int PROTO, bool RANDOM, int WGT>
+// pb_xpage_kernel: the first frame touching page c0 = floor(4096 c0 / flen) = c0 q + floor(c0 r /
+// flen) (q, r = 4096 div / mod flen), exact in 32 bits while c0 r < 2^31 (the host sets
+// xp_fa_hi otherwise)
+__device__ __forceinline__ uint32_t pb_xp_first_frame(const pb_kargs &K, uint32_t c0, uint32_t flen)
+{
+    const uint32_t q = pb_divq(PB_XPG, K.flen), r = PB_XPG - q * flen;
+    return c0 * q + pb_divq(c0 * r, K.flen);
+}
+// ... and for any c0: a double reciprocal with a +-1 fix-up
+__device__ __forceinline__ uint64_t pb_xp_first_frame64(uint32_t c0, uint32_t flen, double inv)
+{
+    const uint64_t p0 = (uint64_t)c0 * PB_XPG;
+    uint64_t fa = (uint64_t)((double)p0 * inv);
+    if (fa * flen > p0)
+        --fa;
+    else if ((fa + 1) * flen <= p0)
+        ++fa;
+    return fa;
+}
+
+template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4 = true> // A4: flen % 4 == 0 (else 2 mod 4)
 __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[]; // K.xs_np page regions
@@ -702,52 +737,52 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
     else
         c0 = K.xs_full * np + (b - K.xs_full) * np, cs = 1;
 
+    // Page c = c0 + i cs starts at byte 4096 c = fa0 flen - rem0 + 4096 cs i: frame fa0 =
+    // floor(4096 c0 / flen) and rem0 = 4096 c0 - fa0 flen are uniform (one 64-bit division
+    // per workgroup), the rest is 32-bit: t = rem0 + 4096 cs i < 2^18, so page i's first frame
+    // is fa0 + t / flen (exact multiply-shift) and slot j starts at byte j flen - t % flen of
+    // the page.  (Per lane, a double reciprocal and 64-bit fix-ups cost ~40 VALU per slot.)
+    const uint32_t fa_lo = pb_xp_first_frame(K, c0, flen);
+    const uint64_t fa0 = K.xp_fa_hi ? pb_xp_first_frame64(c0, flen, K.xp_inv) : (uint64_t)fa_lo;
+    const uint32_t rem0 = (uint32_t)((uint64_t)c0 * PB_XPG - fa0 * flen);
     // at most two slots per 256 lanes (np * fpp <= 512): one straight-line pass per
     // 512-thread workgroup, two unrolled passes per 256-thread one (a loop kept the
     // kernel arguments live across iterations and spilled them through v_readlane /
     // v_writelane, 41 VALU per frame)
-    uint32_t starts = 0; // this lane's frames that start in their page (the counters)
 #pragma unroll
     for (uint32_t pass = 0; pass < 512 / WGT; ++pass)
     {
         const uint32_t sl = tid + pass * WGT;
         if (sl >= np * fpp)
             break;
-        const uint32_t i = pb_divq(sl, K.xp_div), j = sl - i * fpp;
+        const uint32_t i = pb_divq(sl, K.xp_div), j = sl - __umul24(i, fpp);
         const uint32_t c = c0 + i * cs;
         if (c >= K.xs_nch)
             continue;
-        const uint64_t p0 = (uint64_t)c * PB_XPG;
-        uint64_t fa = (uint64_t)((double)p0 * K.xp_inv); // floor(p0 / flen), +-1
-        if (fa * flen > p0)
-            --fa;
-        else if ((fa + 1) * flen <= p0)
-            ++fa;
-        const uint64_t f = fa + j;
-        if (f >= K.n_frames || f * flen >= p0 + PB_XPG)
+        const uint32_t t = rem0 + ((i * cs) << 12);
+        const uint32_t qi = pb_divq(t, K.flen);
+        const int off = (int)__umul24(j, flen) - (int)(t - __umul24(qi, flen)); // (-flen, 4096 + flen)
+        const uint64_t f = fa0 + qi + j;
+        if (off >= (int)PB_XPG || f >= K.n_frames)
             continue;
         uint32_t d[NDW];
         pb_small_frame<NDW, PROTO, RANDOM>(K, f, d, rtab);
-        const int off = (int)((int64_t)(f * flen) - (int64_t)p0); // (-flen, 4096), even
-        starts += off >= 0 ? 1u : 0u;
-        if ((flen & 3u) == 0)
+        if (A4)
         {
+            // 4-B aligned: dword pairs (ds_write2_b32 / ds_write_b64), a last single dword
             uint32_t *row = s_tile + (i * PB_XREG + 128 + off) / 4;
 #pragma unroll
-            for (int t = 0; t < NDW; ++t)
-                if ((uint32_t)(4 * t) < flen)
-                    row[t] = d[t];
+            for (int t2 = 0; t2 < NDW; t2 += 2)
+            {
+                if ((uint32_t)(4 * t2 + 4) < flen)
+                    *reinterpret_cast<pb_u32x2a4 *>(row + t2) = pb_u32x2a4{d[t2], d[t2 + 1]};
+                else if ((uint32_t)(4 * t2) < flen)
+                    row[t2] = d[t2];
+            }
         }
-        else // 2 mod 4 (98-B ICMP, 106-B UDP): a half dword at one end (pb_small_put)
-            pb_small_put<NDW, false>(s_tile, d, i * PB_XREG + 128 + off, flen);
+        else // 2 mod 4 (98-B ICMP, 106-B UDP under PBGPU_XP_FORCE): a half dword at one end
+            pb_small_put<NDW, false, 2>(s_tile, d, i * PB_XREG + 128 + off, flen);
     }
-    // per-wave sums of the frame starts (no init race: one plain write per wave)
-    __shared__ uint32_t s_starts[WGT / 64];
-#pragma unroll
-    for (uint32_t dd = 32; dd > 0; dd >>= 1)
-        starts += __shfl_xor(starts, dd, 64);
-    if ((tid & 63u) == 0)
-        s_starts[tid >> 6] = starts;
     __syncthreads();
 
     // page i -> HBM: one 16-B store per lane per page (256 lanes per page)
@@ -770,18 +805,16 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
     }
     if (tid == 0)
     {
-        // the stored pages, and the frames that start in them (each frame counted once; summed
-        // from the building lanes: 64-bit divisions here on one lane cost the kernel ~45%)
-        uint64_t fr = 0, by = 0;
-        for (uint32_t w = 0; w < WGT / 64; ++w)
-            fr += s_starts[w];
+        // the bytes of the stored pages (fixed length: the host takes frames = bytes / length,
+        // pb_count; counting each page's frame starts cost 4%, profiles/r04/ab)
+        uint64_t by = 0;
         for (uint32_t i = 0; i < np; ++i)
         {
             const uint32_t c = c0 + i * cs;
             if (c < K.xs_nch)
                 by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
         }
-        pb_count(K, b, fr, by);
+        pb_count(K, b, 0, by);
     }
 }
 
@@ -2212,7 +2245,10 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     // walked bytes of one parity, the first walked position having parity par
     constexpr uint32_t SM = (1u << PB_ORB_SH) - 1u, HALF = (SM + 1u) >> 1;
     const bool fp = (p & SM) > HALF, fq = (q & SM) > HALF; // forward to the next sample
-    const uint32_t tp = K.orbit[(p >> PB_ORB_SH) + (fp ? 1u : 0u)], tq = K.orbit[(q >> PB_ORB_SH) + (fq ? 1u : 0u)];
+    // (PBGPU_FST_DBG bit 6, diagnostics: the table entries replaced by their indices, no loads)
+    const uint32_t ip = (p >> PB_ORB_SH) + (fp ? 1u : 0u), iq = (q >> PB_ORB_SH) + (fq ? 1u : 0u);
+    const bool noload = (K.fst_dbg & 64u) != 0;
+    const uint32_t tp = noload ? ip : K.orbit[ip], tq = noload ? iq : K.orbit[iq];
     const uint32_t dp = fp ? SM + 1u - (p & SM) : (p & SM), dq = fq ? SM + 1u - (q & SM) : (q & SM);
     const uint32_t ap_ = fp ? PB_A3 & PB_M24 : PB_A3I, cp_ = fp ? PB_C3 & PB_M24 : PB_C3I;
     const uint32_t aq_ = fq ? PB_A3 & PB_M24 : PB_A3I, cq_ = fq ? PB_C3 & PB_M24 : PB_C3I;
@@ -2265,6 +2301,9 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
 
 #ifndef PB_VL_SPLIT
 #define PB_VL_SPLIT 1
+#endif
+#ifndef PB_VL_LATE
+#define PB_VL_LATE 1 // pb_vline_kernel: the L4 checksum is folded into the header image after the scan
 #endif
 #ifndef PB_VL_IMGW
 #define PB_VL_IMGW 1 // prologue: header images as NHW dword writes, line map as plain writes + the last line
@@ -2345,6 +2384,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
 #pragma unroll
     for (int w = 0; w < 16; ++w)
         d[w] = 0u;
+    uint32_t csum_v = 0; // PB_VL_LATE: the L4 checksum field, ORed into d[] after the scan
     if (valid)
     {
         uint64_t k;
@@ -2367,10 +2407,13 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             // (PBGPU_FST_DBG bit 5, diagnostics: no payload sum, the orbit-table reads skipped)
             const uint32_t ps = (K.fst_dbg & 32u) ? 0u : pb_orbit_sum(K, P.st0, P.plen);
             const uint32_t c = (~pb_fold(pb_fold(hs) + ps)) & 0xFFFFu;
-            const uint32_t cv = K.csum_hi ? (c << 16) : c;
+            csum_v = K.csum_hi ? (c << 16) : c;
+            if (!PB_VL_LATE)
+            {
 #pragma unroll
-            for (uint32_t w = 0; w < 16; ++w)
-                d[w] |= w == K.csum_dw ? cv : 0u;
+                for (uint32_t w = 0; w < 16; ++w)
+                    d[w] |= w == K.csum_dw ? csum_v : 0u;
+            }
         }
     }
     // frame starts: exclusive scan of the slot lengths (in-wave shuffles, wave totals via LDS)
@@ -2429,6 +2472,14 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     const int32_t tix = (int32_t)tid - (int32_t)(GH - ng);
     if (valid && tix >= 0)
     {
+        if (PB_VL_LATE)
+        {
+            // the checksum only now: the orbit-table loads behind it (issued in the frame's
+            // field computation) complete under the scan and the barrier instead of before them
+#pragma unroll
+            for (uint32_t w = 0; w < 16; ++w)
+                d[w] |= w == K.csum_dw ? csum_v : 0u;
+        }
         const uint32_t r = (uint32_t)(start - wbase);
         const uint32_t s0 = r & 15u;
         const uint2 jt = s_jt[s0];
@@ -2795,6 +2846,21 @@ static size_t pb_small_tile_bytes(uint32_t wgt, uint32_t flen)
     return PB_SMALL_DYN ? (((size_t)wgt * flen + 15) & ~(size_t)15) + 32 : 0;
 }
 
+// pb_small_kernel: workgroup b builds frames [wgt b, wgt b + wgt)
+template <int NDW, int PROTO, bool RANDOM, int AL>
+static void pbk_launch_linear(const pb_kargs *K, hipStream_t st)
+{
+    const uint32_t wgt = K->small_wgt ? K->small_wgt : PB_WG;
+    const dim3 g((uint32_t)((K->n_frames + wgt - 1) / wgt));
+    const size_t lds = pb_small_tile_bytes(wgt, K->fixed_len) + K->lds_pad;
+    if (wgt == 64)
+        hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, RANDOM, 64, AL>), g, dim3(64), lds, st, *K);
+    else if (wgt == 128)
+        hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, RANDOM, 128, AL>), g, dim3(128), lds, st, *K);
+    else
+        hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, RANDOM, PB_WG, AL>), g, dim3(PB_WG), lds, st, *K);
+}
+
 template <int NDW, int PROTO>
 static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
 {
@@ -2802,47 +2868,48 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
     {
         const size_t lds = (size_t)K->xs_np * PB_XREG + K->lds_pad;
         const bool w512 = K->xp_wgt == 512;
-        if (K->pl0.random && w512)
-            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, 512>), dim3(K->xs_grid), dim3(512), lds, st, *K);
-        else if (K->pl0.random)
-            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, PB_WG>), dim3(K->xs_grid), dim3(PB_WG), lds, st, *K);
-        else if (w512)
-            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false, 512>), dim3(K->xs_grid), dim3(512), lds, st, *K);
-        else
-            hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false, PB_WG>), dim3(K->xs_grid), dim3(PB_WG), lds, st, *K);
+        const dim3 g(K->xs_grid);
+        if (K->fixed_len % 4 == 0)
+        {
+            if (K->pl0.random && w512)
+                hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, 512>), g, dim3(512), lds, st, *K);
+            else if (K->pl0.random)
+                hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, PB_WG>), g, dim3(PB_WG), lds, st, *K);
+            else if (w512)
+                hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false, 512>), g, dim3(512), lds, st, *K);
+            else
+                hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false, PB_WG>), g, dim3(PB_WG), lds, st, *K);
+        }
+        else // 2 mod 4: only under PBGPU_XP_FORCE (experiments)
+        {
+            if (K->pl0.random && w512)
+                hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, 512, false>), g, dim3(512), lds, st, *K);
+            else if (K->pl0.random)
+                hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, PB_WG, false>), g, dim3(PB_WG), lds, st, *K);
+            else if (w512)
+                hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false, 512, false>), g, dim3(512), lds, st, *K);
+            else
+                hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false, PB_WG, false>), g, dim3(PB_WG), lds, st, *K);
+        }
     }
-    else if (K->pl0.random)
+    else if (K->xs_grid)
     {
-        if (K->xs_grid)
+        if (K->pl0.random)
             hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
         else
-        {
-            const uint32_t wgt = K->small_wgt ? K->small_wgt : PB_WG;
-            const uint32_t g = (uint32_t)((K->n_frames + wgt - 1) / wgt);
-            if (wgt == 64)
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, 64>), dim3(g), dim3(64), pb_small_tile_bytes(64, K->fixed_len) + K->lds_pad, st, *K);
-            else if (wgt == 128)
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, 128>), dim3(g), dim3(128), pb_small_tile_bytes(128, K->fixed_len) + K->lds_pad, st, *K);
-            else
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, true, PB_WG>), dim3(g), dim3(PB_WG), pb_small_tile_bytes(PB_WG, K->fixed_len) + K->lds_pad, st, *K);
-        }
-    }
-    else
-    {
-        if (K->xs_grid)
             hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
-        else
-        {
-            const uint32_t wgt = K->small_wgt ? K->small_wgt : PB_WG;
-            const uint32_t g = (uint32_t)((K->n_frames + wgt - 1) / wgt);
-            if (wgt == 64)
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, 64>), dim3(g), dim3(64), pb_small_tile_bytes(64, K->fixed_len) + K->lds_pad, st, *K);
-            else if (wgt == 128)
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, 128>), dim3(g), dim3(128), pb_small_tile_bytes(128, K->fixed_len) + K->lds_pad, st, *K);
-            else
-                hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, false, PB_WG>), dim3(g), dim3(PB_WG), pb_small_tile_bytes(PB_WG, K->fixed_len) + K->lds_pad, st, *K);
-        }
     }
+    else if (K->fixed_len % 4 == 2) // 98-B ICMP, 106-B UDP: only the 2-mod-4 tile writes compiled in
+    {
+        if (K->pl0.random)
+            pbk_launch_linear<NDW, PROTO, true, 2>(K, st);
+        else
+            pbk_launch_linear<NDW, PROTO, false, 2>(K, st);
+    }
+    else if (K->pl0.random)
+        pbk_launch_linear<NDW, PROTO, true, 0>(K, st);
+    else
+        pbk_launch_linear<NDW, PROTO, false, 0>(K, st);
 }
 
 template <int NDW>

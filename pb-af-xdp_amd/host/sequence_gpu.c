@@ -422,7 +422,7 @@ static void *gpu_worker(void *p)
             }
         }
         rc = pb_xsk_open(&xsk, w->device, q, umem_base, nslots, PB_FRAME_SIZE, bf, shared_fd, slot_base,
-                         w->shared ? umem_frames : nslots);
+                         w->shared ? umem_frames : nslots, w->cmd.queue_set ? (uint32_t)w->cmd.queue : 0u);
         if (w->shared && w->shard == 0)
         {
             pthread_mutex_lock(&w->shared->mu);
@@ -697,6 +697,15 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
         t_cnt = PB_MAX_WORKERS - worker_cnt;
     start_time[idx] = time(NULL);
     shared_umem_t *shared = NULL;
+    if (cmd.shared_umem && cmd.queue_set && t_cnt > 1 && cmd.tx && strcmp(cmd.tx, "xsk") == 0)
+    {
+        /* every thread on one queue: their sockets would have to share the owner's fill /
+         * completion rings (pb_xsk_open); refuse instead of failing threads 1..n-1 at bind */
+        fprintf(stderr, "[%d] --sharedumem with --queue binds all %d threads to queue %d: use one thread, or "
+                        "drop --queue (thread t then takes queue t).\n", idx + 1, t_cnt, cmd.queue);
+        last_error = PBGPU_EINVAL;
+        return;
+    }
     if (cmd.shared_umem && t_cnt > 0)
     {
         /* one UMEM for the sequence's threads (af_xdp.c:412-428), each its own power-of-two

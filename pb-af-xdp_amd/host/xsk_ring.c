@@ -199,10 +199,17 @@ static int map_ring(int fd, pb_xsk_ring_t *r, const struct xdp_ring_offset *off,
 }
 
 int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, uint32_t n_frames,
-                uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames)
+                uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames,
+                uint32_t shared_queue)
 {
     if (x == NULL || ifname == NULL || umem == NULL || n_frames == 0 || (n_frames & (n_frames - 1)) ||
         slot_base + n_frames > (umem_frames ? umem_frames : n_frames))
+        return -EINVAL;
+    /* xsk_bind: XDP_SHARED_UMEM on the owner's (device, queue) shares its buffer pool and
+     * rejects a socket with fill / completion rings of its own; these per-thread rings need
+     * another queue (libxdp's xsk_socket__create_shared handles the same-queue case by
+     * sharing the owner's rings between sockets, which this reaper does not) */
+    if (shared_fd >= 0 && shared_queue == queue)
         return -EINVAL;
     memset(x, 0, sizeof *x);
     x->fd = -1;

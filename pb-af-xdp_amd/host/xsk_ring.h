@@ -101,10 +101,15 @@ uint32_t pb_xsk_loop_consume(pb_xsk_t *x, uint32_t max, pb_xsk_sink_fn sink, voi
  * (af_xdp.c:289-330).  shared_fd >= 0: the UMEM is already registered on that
  * socket (--sharedumem, af_xdp.c:412-428): this socket binds with
  * XDP_SHARED_UMEM and its own fill / completion rings, and uses the n_frames
- * slots from slot_base on.  Returns 0, or -errno (EPERM without CAP_NET_RAW,
- * EAFNOSUPPORT without AF_XDP). */
+ * slots from slot_base on.  shared_queue: the queue the owner socket is bound
+ * to.  The kernel lets a shared-UMEM socket keep rings of its own only on
+ * another queue (or device); on the owner's queue it must use the owner's
+ * fill / completion rings, which a per-thread reaper cannot share, so that
+ * case is refused with -EINVAL before any socket is made.  Returns 0, or
+ * -errno (EPERM without CAP_NET_RAW, EAFNOSUPPORT without AF_XDP). */
 int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, uint32_t n_frames,
-                uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames);
+                uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames,
+                uint32_t shared_queue);
 void pb_xsk_close(pb_xsk_t *x);
 
 /* complete_tx() (af_xdp.c:25-53): wake the kernel if it asks (or always without

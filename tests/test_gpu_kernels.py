@@ -325,6 +325,41 @@ def test_vline_workgroup_sizes(ctx, monkeypatch, wgf):
         assert kern.startswith("pb_vline_kernel<"), kern
 
 
+def test_vline_offsets_across_4gib_boundaries(ctx, monkeypatch):
+    """pb_vline_kernel keeps each frame's offset as its low 32 bits plus its region's 64-bit
+    start (pb_expand_offsets rebuilds offset = rstart + (u32)(low - (u32)rstart)): a build of
+    2^23 configs[2] frames (~6.9 GB) crosses 2^32 and 2^33, so the offsets must equal
+    pb_vstage_kernel's 64-bit ones everywhere, and the frames around each 2^32 multiple must
+    be the oracle's bytes at the oracle's offsets."""
+    seq = Sequence.from_config(pc.get("c3_udp_var"))
+    n, first = 1 << 23, 12345
+    offs = {}
+    for kernel in ("vline", "vstage"):
+        if kernel == "vstage":
+            monkeypatch.setenv("PBGPU_KERNEL", "vstage")
+        ctx.load_sequence(6, seq, pc.SEED_BASE)
+        fb = ctx.alloc_frames(*ctx.build_size(6, n))
+        ctx.build(6, first, n, fb)
+        ctx.sync()
+        offs[kernel] = fb.offsets()
+        name = ctx.kernel_name(6)
+        if kernel == "vline":
+            assert name.startswith("pb_vline_kernel")
+            data = fb.packed()
+        else:
+            assert name.startswith("pb_vstage_kernel")
+        fb.free()
+    o = offs["vline"]
+    assert o[-1] > (1 << 33)  # the build crosses two 4-GiB boundaries
+    assert np.array_equal(o, offs["vstage"])
+    for k in range(1, int(o[-1] >> 32) + 1):
+        f = int(np.searchsorted(o, k << 32, side="right")) - 1  # the frame holding byte k * 2^32
+        f0 = max(0, f - 16)
+        od, oo = ob.build(seq, 6, first + f0, 32, pc.SEED_BASE)
+        assert np.array_equal(o[f0:f0 + 33] - o[f0], oo), k
+        assert np.array_equal(data[int(o[f0]):int(o[f0 + 32])], od), k
+
+
 def test_vline_matches_vstage_at_size(ctx, monkeypatch):
     """configs[2] at 2^22 frames: the two variable-length kernels build the same bytes."""
     seq = Sequence.from_config(pc.get("c3_udp_var"))

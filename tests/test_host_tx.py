@@ -144,14 +144,31 @@ def test_af_xdp_socket_setup_fails_cleanly_without_privilege(libs):
     x = Xsk()
     umem = np.zeros(4096 * 4096 + 4096, dtype=np.uint8)
     base = (umem.ctypes.data + 4095) & ~4095
-    rc = host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096)
+    rc = host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096, 0)
     # a negative errno (no AF_XDP / CAP_NET_RAW in this container), or a bound socket
     assert rc <= 0
     if rc == 0:
         host.pb_xsk_close(C.byref(x))
-    assert host.pb_xsk_open(C.byref(x), b"pbnodev0", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096) == -19  # -ENODEV
+    assert host.pb_xsk_open(C.byref(x), b"pbnodev0", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096, 0) == -19  # -ENODEV
     # a shared-UMEM socket's slot range must lie inside the UMEM
-    assert host.pb_xsk_open(C.byref(x), b"lo", 1, C.c_void_p(base), 2048, 4096, 0, 3, 4096, 4096) == -22
+    assert host.pb_xsk_open(C.byref(x), b"lo", 1, C.c_void_p(base), 2048, 4096, 0, 3, 4096, 4096, 0) == -22
+
+
+def test_shared_umem_socket_on_the_owners_queue_is_refused(libs):
+    """xsk_bind lets an XDP_SHARED_UMEM socket keep its own fill / completion rings only
+    on another queue or device; on the owner's queue it must take the owner's rings
+    (a shared buffer pool), which per-thread reapers cannot share.  pb_xsk_open refuses
+    that combination up front, and seq_send refuses --sharedumem --queue with several
+    threads instead of letting threads 1..n-1 fail at bind."""
+    host, _ = libs
+    x = Xsk()
+    umem = np.zeros(4096 * 4096 + 4096, dtype=np.uint8)
+    base = (umem.ctypes.data + 4095) & ~4095
+    # a valid slot range (2048 slots from 2048 of 4096), shared fd, the owner's queue 5
+    assert host.pb_xsk_open(C.byref(x), b"lo", 5, C.c_void_p(base), 2048, 4096, 0, 3, 2048, 4096, 5) == -22
+    assert x.fd == 0 and x.umem is None  # refused before any socket was made
+    r = _run(libs, _cfg(maxpckts=1000, delay=0, threads=2), shared_umem=1, queue=5, queue_set=1, tx=b"xsk")
+    assert r["err"] == -22 and r["seen"] == 0 and r["pckts"] == 0
 
 
 # ---------------------------------------------------------------- worker loop
