@@ -161,6 +161,9 @@ struct pb_kargs
     // pb_xpage_kernel: 1 when the launch's last page index times 4096 % flen reaches 2^31 (the
     // first frame of a page then takes the 64-bit path)
     uint32_t xp_fa_hi;
+    // pb_xcd_region's block size for the region-walking kernels: 0 = each XCD walks one
+    // contiguous eighth of the launch, sh > 0 = blocks of 2^sh regions dealt to the XCDs in turn
+    uint32_t xcd_sh;
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

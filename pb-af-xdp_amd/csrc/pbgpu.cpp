@@ -1358,6 +1358,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         fe->land_pending = false;
     }
     pb_kargs K = S.K;
+    K.xcd_sh = (uint32_t)env_int("PBGPU_XCD_SH", 0); // (experiments) pb_xcd_region block size
     K.first_iter = first_iter;
     K.n_frames = nf;
     K.out = out->data;

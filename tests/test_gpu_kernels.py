@@ -328,7 +328,7 @@ def test_vline_workgroup_sizes(ctx, monkeypatch, wgf):
 def test_vline_offsets_across_4gib_boundaries(ctx, monkeypatch):
     """pb_vline_kernel keeps each frame's offset as its low 32 bits plus its region's 64-bit
     start (pb_expand_offsets rebuilds offset = rstart + (u32)(low - (u32)rstart)): a build of
-    2^23 configs[2] frames (~6.9 GB) crosses 2^32 and 2^33, so the offsets must equal
+    2^23 configs[2] frames (~6.9 GB) crosses 2^32, so the offsets must equal
     pb_vstage_kernel's 64-bit ones everywhere, and the frames around each 2^32 multiple must
     be the oracle's bytes at the oracle's offsets."""
     seq = Sequence.from_config(pc.get("c3_udp_var"))
@@ -350,7 +350,7 @@ def test_vline_offsets_across_4gib_boundaries(ctx, monkeypatch):
             assert name.startswith("pb_vstage_kernel")
         fb.free()
     o = offs["vline"]
-    assert o[-1] > (1 << 33)  # the build crosses two 4-GiB boundaries
+    assert o[-1] > (1 << 32)  # the build crosses a 4-GiB boundary
     assert np.array_equal(o, offs["vstage"])
     for k in range(1, int(o[-1] >> 32) + 1):
         f = int(np.searchsorted(o, k << 32, side="right")) - 1  # the frame holding byte k * 2^32
