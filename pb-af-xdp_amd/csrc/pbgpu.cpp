@@ -871,6 +871,10 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             while ((minf << K.xs_fp_shift) < 4096)
                 ++K.xs_fp_shift;
             K.xs_np = 256 >> K.xs_fp_shift;
+            // (experiments) PBGPU_XS_WGT = 64 / 128: one / two 4 KiB pages per 64-B-frame workgroup
+            const int xw = env_int("PBGPU_XS_WGT", 256);
+            if (K.small_ndw == 16 && (xw == 64 || xw == 128))
+                K.xs_np = (uint32_t)xw >> K.xs_fp_shift;
         }
         else if ((minf % 4 == 0 || (minf % 2 == 0 && xp_force)) &&
                  ((minf <= 64 && 2 * PB_WG / ((4096 + minf - 1) / minf + 1) >= 6) || xp_force) &&

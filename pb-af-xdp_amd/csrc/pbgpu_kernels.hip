@@ -632,10 +632,10 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
 // frames in both owners measured slower than the linear form (60-B TCP 0.37 vs
 // 0.345 ms, 98-B ICMP 0.70 vs 0.64), so they keep pb_small_kernel.
 
-template <int NDW, int PROTO, bool RANDOM>
-__global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
+template <int NDW, int PROTO, bool RANDOM, int WGT = PB_WG> // 64-B frames: WGT / 64 pages per workgroup
+__global__ __launch_bounds__(WGT) void pb_xsmall_kernel(pb_kargs K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_tile[(NDW == 16 ? 4 : PB_XNP_MAX) * PB_XREG / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[(NDW == 16 ? WGT / 64 : PB_XNP_MAX) * PB_XREG / 4];
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
     const uint32_t flen = K.fixed_len;
     const uint32_t np = K.xs_np;
@@ -665,15 +665,17 @@ __global__ __launch_bounds__(PB_WG) void pb_xsmall_kernel(pb_kargs K)
     }
     __syncthreads();
 
-    // page i -> HBM: one 16-B store per lane per page
+    // page i -> HBM: 256 / WGT 16-B stores per lane per page (one at 256 threads)
+    constexpr uint32_t NPG = NDW == 16 ? (uint32_t)WGT / 64u : PB_XNP_MAX, SPP = 256u / WGT;
 #pragma unroll
-    for (uint32_t i = 0; i < (NDW == 16 ? 4u : PB_XNP_MAX); ++i)
+    for (uint32_t u = 0; u < NPG * SPP; ++u)
     {
+        const uint32_t i = u / SPP, ch = (u % SPP) * WGT + tid;
         const uint32_t c = c0 + i * cs;
-        const uint64_t o = (uint64_t)c * PB_XPG + 16 * tid;
+        const uint64_t o = (uint64_t)c * PB_XPG + 16 * ch;
         if (i < np && c < K.xs_nch && o < T)
         {
-            const uint32_t sl = (i * PB_XREG + 128) / 16 + tid;
+            const uint32_t sl = (i * PB_XREG + 128) / 16 + ch;
             pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[pb_swz(sl)];
             if (o + 16 > T) // last chunk of the stream: zero the tail
             {
@@ -2932,10 +2934,20 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
     }
     else if (K->xs_grid)
     {
-        if (K->pl0.random)
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
+        const dim3 g(K->xs_grid);
+        const uint32_t w = NDW == 16 ? (K->xs_np << K->xs_fp_shift) : PB_WG; // 64 / 128 / 256 threads
+        if (K->pl0.random && w == 64)
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true, 64>), g, dim3(64), K->lds_pad, st, *K);
+        else if (K->pl0.random && w == 128)
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true, 128>), g, dim3(128), K->lds_pad, st, *K);
+        else if (K->pl0.random)
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), g, dim3(PB_WG), K->lds_pad, st, *K);
+        else if (w == 64)
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false, 64>), g, dim3(64), K->lds_pad, st, *K);
+        else if (w == 128)
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false, 128>), g, dim3(128), K->lds_pad, st, *K);
         else
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false>), g, dim3(PB_WG), K->lds_pad, st, *K);
     }
     else if (K->fixed_len % 4 == 2) // 98-B ICMP, 106-B UDP: only the 2-mod-4 tile writes compiled in
     {
