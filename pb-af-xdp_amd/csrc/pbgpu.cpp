@@ -27,6 +27,9 @@
 #include "pb_device.h"
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st);
+extern "C" uint32_t pbk_build_grid(const pb_kargs *K);
+extern "C" hipError_t pbk_launch_ctr_fold(const uint32_t *slots, uint64_t n, uint32_t pairs,
+                                          unsigned long long *counters, hipStream_t st);
 extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
                                          uint64_t *offsets, hipStream_t st);
 extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t wgf, uint32_t *bsum, uint32_t nblk,
@@ -106,6 +109,12 @@ struct seq_slot
     pb_pl *d_pls = nullptr;
     uint32_t *d_lit_stop = nullptr;
     uint8_t *d_blob = nullptr;
+    // per-workgroup counts of the launches not yet folded into the counters (pb_count): a
+    // linear ring of u32 words, folded (pb_ctr_fold) when full, on reload and by pbgpu_counters
+    uint32_t *d_ctr_slots = nullptr;
+    uint64_t ctr_cap = 0, ctr_used = 0, ctr_pairs = 1; // words; words per record
+    hipStream_t ctr_last = nullptr; // the stream of the last launch that wrote or folded the ring
+    hipEvent_t ctr_ev = nullptr;
 };
 
 struct timing_pair
@@ -461,6 +470,50 @@ static int join_builds(pbgpu_ctx *ctx)
 
 static void slot_counts(const pbgpu_ctx *ctx, const unsigned long long *h, int i, uint64_t *p, uint64_t *b);
 
+// Launches that touch a sequence's count ring (its builds and folds) run in order, whatever
+// stream each is issued on: the next one waits for the previous one's stream.
+static int ctr_order(seq_slot &S, hipStream_t st)
+{
+    if (S.ctr_last && S.ctr_last != st)
+    {
+        if (S.ctr_ev == nullptr)
+            HIPCHK(hipEventCreateWithFlags(&S.ctr_ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(S.ctr_ev, S.ctr_last));
+        HIPCHK(hipStreamWaitEvent(st, S.ctr_ev, 0));
+    }
+    S.ctr_last = st;
+    return PBGPU_OK;
+}
+
+// Adds the records of slot i's launches since the last fold into its counters (on st).
+static int ctr_fold(pbgpu_ctx *ctx, int i, hipStream_t st)
+{
+    seq_slot &S = ctx->seqs[i];
+    if (S.ctr_used == 0)
+        return PBGPU_OK;
+    const int rc = ctr_order(S, st);
+    if (rc != PBGPU_OK)
+        return rc;
+    HIPCHK(pbk_launch_ctr_fold(S.d_ctr_slots, S.ctr_used / S.ctr_pairs, (uint32_t)S.ctr_pairs,
+                               ctx->d_counters + PB_CTR_WORDS * (size_t)i, st));
+    S.ctr_used = 0;
+    return PBGPU_OK;
+}
+
+static void ctr_free(seq_slot &S)
+{
+    if (S.d_ctr_slots)
+        (void)hipFree(S.d_ctr_slots);
+    if (S.ctr_ev)
+        (void)hipEventDestroy(S.ctr_ev);
+    S.d_ctr_slots = nullptr;
+    S.ctr_ev = nullptr;
+    S.ctr_cap = S.ctr_used = 0;
+    S.ctr_last = nullptr;
+}
+
+#define PB_CTR_RING_WORDS (8ull << 20) // count ring per sequence: 32 MiB, 64 launches of 2^25 64-B frames
+
 #define PB_JOIN(ctx)                         \
     do                                       \
     {                                        \
@@ -531,7 +584,10 @@ void pbgpu_close(pbgpu_ctx *ctx)
     for (hipEvent_t e : ctx->land_pool)
         (void)hipEventDestroy(e);
     for (auto &s : ctx->seqs)
+    {
+        ctr_free(s);
         slot_free(s);
+    }
     for (auto &p : ctx->pending)
         ctx->pool.push_back(p);
     for (auto &p : ctx->pool)
@@ -582,6 +638,11 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         return PBGPU_EINVAL;
     HIPCHK(hipSetDevice(ctx->device));
     PB_JOIN(ctx);
+    {
+        const int frc = ctr_fold(ctx, seq_idx, ctx->stream); // the old sequence's pending counts
+        if (frc != PBGPU_OK)
+            return frc;
+    }
     HIPCHK(hipStreamSynchronize(ctx->stream)); // no build still reads the slot's tables
     seq_slot &S = ctx->seqs[seq_idx];
     if (S.loaded) // the slot's counts so far (their frames follow the old sequence's length)
@@ -595,7 +656,17 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         ctx->ctr_base[seq_idx][1] = b;
         HIPCHK(hipMemset(dc, 0, h.size() * sizeof(h[0])));
     }
-    slot_free(S);
+    {
+        // the count ring (empty now) stays with the slot
+        uint32_t *ring = S.d_ctr_slots;
+        const uint64_t cap = S.ctr_cap;
+        hipEvent_t ev = S.ctr_ev;
+        slot_free(S);
+        S.d_ctr_slots = ring;
+        S.ctr_cap = cap;
+        S.ctr_ev = ev;
+        S.ctr_last = ctx->stream;
+    }
 
     pb_rules_t R = {PB_PAYLOAD_STREAM, PB_FOLD_FULL};
     if (rules)
@@ -1433,11 +1504,42 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             const uint32_t np = K.xs_np;
             K.xs_full = (uint32_t)(nch / (8 * np) * 8);
             K.xs_grid = K.xs_full + (uint32_t)((nch - (uint64_t)K.xs_full * np + np - 1) / np);
-            K.xp_fa_hi = K.xp && (uint64_t)nch * (4096 % K.fixed_len) >= (1ull << 31);
+            // (PBGPU_XP_FA64=1: the 64-bit path at any size, so the tests reach it)
+            K.xp_fa_hi = K.xp && ((uint64_t)nch * (4096 % K.fixed_len) >= (1ull << 31) || env_is("PBGPU_XP_FA64", "1"));
         }
     }
-    timing_pair tp = {nullptr, nullptr};
+    // this launch's per-workgroup count records (pb_count): the next words of the sequence's
+    // ring, folded into the counters first when it is full (PBGPU_CTR_ATOMIC=1: one atomic per
+    // workgroup instead)
     int rc = PBGPU_OK;
+    K.ctr_slots = nullptr;
+    if (!env_is("PBGPU_CTR_ATOMIC", "1"))
+    {
+        const uint64_t pairs = K.fixed_len ? 1 : 2;
+        const uint64_t words = (uint64_t)pbk_build_grid(&K) * pairs;
+        if (S.ctr_pairs != pairs || S.ctr_used + words > S.ctr_cap)
+        {
+            if ((rc = ctr_fold(ctx, seq_idx, st)) != PBGPU_OK)
+                return rc;
+            S.ctr_pairs = pairs;
+            if (words > S.ctr_cap)
+            {
+                HIPCHK(hipStreamSynchronize(st)); // the old ring's fold has read it
+                if (S.d_ctr_slots)
+                    (void)hipFree(S.d_ctr_slots);
+                S.d_ctr_slots = nullptr;
+                S.ctr_cap = 0;
+                const uint64_t cap = words > PB_CTR_RING_WORDS ? words : PB_CTR_RING_WORDS;
+                HIPCHK(hipMalloc((void **)&S.d_ctr_slots, cap * sizeof(uint32_t)));
+                S.ctr_cap = cap;
+            }
+        }
+        if ((rc = ctr_order(S, st)) != PBGPU_OK)
+            return rc;
+        K.ctr_slots = S.d_ctr_slots + S.ctr_used;
+        S.ctr_used += words;
+    }
+    timing_pair tp = {nullptr, nullptr};
     if (!span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
         return rc;
     const bool timing = (K.stage_win || K.fst_g) && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
@@ -1856,7 +1958,13 @@ int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)
     PB_JOIN(ctx);
     if (n_seq == 0)
         return PBGPU_OK;
-    // the kernels' per-workgroup adds land in PB_CTR_SHARDS shards per sequence: sum them
+    // the launches' pending per-workgroup records first, then the shards' sums
+    for (int i = 0; i < n_seq; ++i)
+    {
+        const int frc = ctr_fold(ctx, i, ctx->stream);
+        if (frc != PBGPU_OK)
+            return frc;
+    }
     std::vector<unsigned long long> h(PB_CTR_WORDS * (size_t)n_seq);
     HIPCHK(hipMemcpyAsync(h.data(), ctx->d_counters, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -347,23 +347,87 @@ __device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg, uint
     return 8u * full + x * r + (j - full);
 }
 
-// The reference's total_pckts / total_bytes (sequence.c:633-642), counted as work is done:
-// each workgroup adds the frames it built and the bytes it stored (so a skipped store or a
-// short build shows in pbgpu_counters), into shard b % PB_CTR_SHARDS of its sequence — one
-// 128-B line per shard, so neighbouring workgroups' adds do not queue on one address.
-// Fixed-length sequences add only the bytes (one atomic per workgroup; the host takes frames =
-// bytes / length): each device-scope atomic is a memory-side transaction.
+// The reference's total_pckts / total_bytes (sequence.c:633-642), counted as work is done: each
+// workgroup records the frames it built and the bytes it stored, so a skipped store or a short
+// build shows in pbgpu_counters.  The record is a plain store into this launch's slot array
+// (K.ctr_slots, one u32 of bytes per workgroup for fixed-length sequences, whose frames the host
+// takes as bytes / length; {frames, bytes} otherwise), at the workgroup's XCD-contiguous position
+// so each XCD's records fill whole lines; pb_ctr_fold adds a run of launches' records into the
+// counters.  A device-scope atomic per workgroup instead executes at the memory side as its own
+// 64-B request: 0.4% of a 64-B launch's HBM traffic (profiles/pmc_r03.json).  Without a slot array
+// (K.ctr_slots null) the workgroup adds to shard b % PB_CTR_SHARDS (one 128-B line per shard).
 #ifndef PB_COUNT
-#define PB_COUNT 1 // (A/B builds) 0: no counter atomics (wrong counters; measures their cost)
+#define PB_COUNT 1 // (A/B builds) 0: no counting at all (wrong counters; measures its cost)
 #endif
 __device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t frames, uint64_t bytes)
 {
     if (!PB_COUNT)
         return;
+    if (K.ctr_slots)
+    {
+        const uint32_t pos = pb_xcd_region(blockIdx.x, gridDim.x);
+        if (K.fixed_len)
+            K.ctr_slots[pos] = (uint32_t)bytes;
+        else
+            reinterpret_cast<uint2 *>(K.ctr_slots)[pos] = make_uint2((uint32_t)frames, (uint32_t)bytes);
+        return;
+    }
     unsigned long long *c = K.counters + (uint64_t)(b % PB_CTR_SHARDS) * PB_CTR_STRIDE;
     if (!K.fixed_len)
         atomicAdd(c, (unsigned long long)frames);
     atomicAdd(c + 1, (unsigned long long)bytes);
+}
+
+// Folds n workgroup records (pb_count's slot array; pairs = 2: {frames, bytes}, 1: bytes only)
+// into a sequence's counters: a grid-stride sum, one atomic pair per workgroup.
+__global__ __launch_bounds__(256) void pb_ctr_fold(const uint32_t *slots, uint64_t n, uint32_t pairs,
+                                                   unsigned long long *counters)
+{
+    uint64_t fr = 0, by = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    {
+        if (pairs == 2)
+        {
+            const uint2 v = reinterpret_cast<const uint2 *>(slots)[i];
+            fr += v.x;
+            by += v.y;
+        }
+        else
+            by += slots[i];
+    }
+#pragma unroll
+    for (uint32_t dd = 32; dd > 0; dd >>= 1)
+    {
+        fr += __shfl_xor(fr, dd, 64);
+        by += __shfl_xor(by, dd, 64);
+    }
+    __shared__ unsigned long long s_sum[2][4];
+    if ((threadIdx.x & 63u) == 0)
+    {
+        s_sum[0][threadIdx.x >> 6] = fr;
+        s_sum[1][threadIdx.x >> 6] = by;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        fr = s_sum[0][0] + s_sum[0][1] + s_sum[0][2] + s_sum[0][3];
+        by = s_sum[1][0] + s_sum[1][1] + s_sum[1][2] + s_sum[1][3];
+        unsigned long long *c = counters + (uint64_t)(blockIdx.x % PB_CTR_SHARDS) * PB_CTR_STRIDE;
+        if (fr)
+            atomicAdd(c, fr);
+        if (by)
+            atomicAdd(c + 1, by);
+    }
+}
+
+extern "C" hipError_t pbk_launch_ctr_fold(const uint32_t *slots, uint64_t n, uint32_t pairs,
+                                          unsigned long long *counters, hipStream_t st)
+{
+    if (n == 0)
+        return hipSuccess;
+    const uint64_t g = (n + 4095) / 4096 < 1024 ? (n + 4095) / 4096 : 1024;
+    hipLaunchKernelGGL(pb_ctr_fold, dim3((uint32_t)g), dim3(256), 0, st, slots, n, pairs, counters);
+    return hipGetLastError();
 }
 
 // ---------------- small fixed-length frames: one lane per frame ----------------
@@ -2273,7 +2337,9 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     uint32_t y = fp ? yp : __umul24(yp, PB_A3I) + PB_C3I; // backward: from position p - 1
     uint32_t z = fq ? yq : __umul24(yq, PB_A3I) + PB_C3I;
     uint32_t ap[2] = {0u, 0u}, aq[2] = {0u, 0u};
-#if PB_ORB_DOT4
+    // (PBGPU_FST_DBG bit 7 flips PB_ORB_DOT4 at run time: a same-placement A/B, correct output)
+    if (PB_ORB_DOT4 ^ ((K.fst_dbg >> 7) & 1u))
+    {
     // four walked bytes per step group: packed into one dword (bytes t = 4g .. 4g + 3), masked to
     // the walk's length, summed by parity with two v_dot4_u32_u8 (13 instead of 20 VALU per group)
     static_assert(HALF % 4 == 0, "walk groups");
@@ -2293,7 +2359,9 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
         y = __umul24(y3, ap_) + cp_;
         z = __umul24(z3, aq_) + cq_;
     }
-#else
+    }
+    else
+    {
 #pragma unroll
     for (uint32_t t = 0; t < HALF; ++t)
     {
@@ -2302,7 +2370,7 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
         y = __umul24(y, ap_) + cp_;
         z = __umul24(z, aq_) + cq_;
     }
-#endif
+    }
     // even / odd position sums of the walked bytes (the first walked position: p, or p - 1)
     const uint32_t pp = fp ? p & 1u : (p & 1u) ^ 1u, pq = fq ? q & 1u : (q & 1u) ^ 1u;
     const uint32_t sEp = ap[pp], sOp = ap[pp ^ 1u], sEq = aq[pq], sOq = aq[pq ^ 1u];
@@ -2425,6 +2493,8 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     for (int w = 0; w < 16; ++w)
         d[w] = 0u;
     uint32_t csum_v = 0; // PB_VL_LATE: the L4 checksum field, ORed into d[] after the scan
+    // (PBGPU_FST_DBG bit 8 flips PB_VL_LATE at run time: a same-placement A/B, correct output)
+    const bool vl_late = (PB_VL_LATE ^ ((K.fst_dbg >> 8) & 1u)) != 0;
     if (valid)
     {
         uint64_t k;
@@ -2448,7 +2518,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             const uint32_t ps = (K.fst_dbg & 32u) ? 0u : pb_orbit_sum(K, P.st0, P.plen);
             const uint32_t c = (~pb_fold(pb_fold(hs) + ps)) & 0xFFFFu;
             csum_v = K.csum_hi ? (c << 16) : c;
-            if (!PB_VL_LATE)
+            if (!vl_late)
             {
 #pragma unroll
                 for (uint32_t w = 0; w < 16; ++w)
@@ -2512,7 +2582,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     const int32_t tix = (int32_t)tid - (int32_t)(GH - ng);
     if (valid && tix >= 0)
     {
-        if (PB_VL_LATE)
+        if (vl_late)
         {
             // the checksum only now: the orbit-table loads behind it (issued in the frame's
             // field computation) complete under the scan and the barrier instead of before them
@@ -2971,6 +3041,26 @@ static void pbk_launch_small(const pb_kargs *K, uint32_t grid, hipStream_t st)
         pbk_launch_small_p<NDW, 6>(K, grid, st);
     else
         pbk_launch_small_p<NDW, 1>(K, grid, st);
+}
+
+// The workgroups pbk_launch_build launches for K (pb_count's records per launch)
+extern "C" uint32_t pbk_build_grid(const pb_kargs *K)
+{
+    const uint64_t n = K->n_frames;
+    uint64_t per = 0;
+    if (K->vl)
+        per = K->vl_wgf;
+    else if (K->fst_g)
+        per = K->fst_wgf;
+    else if (K->gpf_g && !K->stage_win)
+        per = K->gpf_fpw;
+    else if (K->stage_win)
+        per = K->stage_wgf;
+    else if (K->small_ndw && K->xs_grid)
+        return K->xs_grid;
+    else if (K->small_ndw)
+        per = K->small_wgt ? K->small_wgt : PB_WG;
+    return per ? (uint32_t)((n + per - 1) / per) : 0u;
 }
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
