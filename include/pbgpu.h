@@ -175,6 +175,9 @@ int pbgpu_kernel_times(pbgpu_ctx *ctx, double *ms_each, uint32_t cap, uint32_t *
 #define PBGPU_FILL_SHAPES 15
 int pbgpu_fill_probe(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_launch);
 int pbgpu_fill_probe_ex(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_shape, int *best_shape);
+/* The same shapes over the caller's device buffer `dst` (e.g. a pbgpu_frames data buffer): the
+ * write rate of each shape at that buffer's physical placement. */
+int pbgpu_fill_probe_at(pbgpu_ctx *ctx, void *dst, uint64_t bytes, uint32_t reps, double *ms_per_shape);
 const char *pbgpu_fill_shape_name(int shape);
 
 /* Name of the frame-build kernel variant a loaded sequence launches

@@ -132,8 +132,7 @@ struct pb_kargs
                             // pb_vline_kernel: bit 0 the stream, bit 2 its arithmetic (constant stores),
                             // bit 4 the prologue (constant stores over the launch's regions), bit 5
                             // the payload sums (no orbit-table reads), bit 6 the orbit-table reads
-                            // alone (sums computed from the entries' indices); bits 7 / 8 flip
-                            // PB_ORB_DOT4 / PB_VL_LATE (correct output, same-buffer A/B);
+                            // alone (sums computed from the entries' indices);
                             // pb_vstage_kernel: bit 4 fixed 8-lane groups, bit 5 no 32-lane groups, bit 6 workgroup
                             // edges at frame starts, bit 8 no longest-first window order (A/B)
     uint32_t lds_pad;       // dynamic LDS added to the build launch: caps workgroups per CU (fewer
@@ -162,9 +161,9 @@ struct pb_kargs
     // pb_xpage_kernel: 1 when the launch's last page index times 4096 % flen reaches 2^31 (the
     // first frame of a page then takes the 64-bit path)
     uint32_t xp_fa_hi;
-    // pb_xcd_region's block size for the region-walking kernels: 0 = each XCD walks one
-    // contiguous eighth of the launch, sh > 0 = blocks of 2^sh regions dealt to the XCDs in turn
-    uint32_t xcd_sh;
+    // (experiments) pb_xcd_region's rotation for the region-walking kernels: XCD x starts its
+    // contiguous eighth x * xcd_rot / 256 of an eighth in (0: at its first region)
+    uint32_t xcd_rot;
     // this launch's per-workgroup counts (pb_count): u32 bytes per workgroup for fixed-length
     // sequences, {frames, bytes} for variable ones, at position pb_xcd_region(blockIdx.x); the
     // host folds them into `counters` (pb_ctr_fold).  Null: one atomic per workgroup instead.

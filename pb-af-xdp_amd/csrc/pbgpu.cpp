@@ -942,10 +942,6 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             while ((minf << K.xs_fp_shift) < 4096)
                 ++K.xs_fp_shift;
             K.xs_np = 256 >> K.xs_fp_shift;
-            // (experiments) PBGPU_XS_WGT = 64 / 128: one / two 4 KiB pages per 64-B-frame workgroup
-            const int xw = env_int("PBGPU_XS_WGT", 256);
-            if (K.small_ndw == 16 && (xw == 64 || xw == 128))
-                K.xs_np = (uint32_t)xw >> K.xs_fp_shift;
         }
         else if ((minf % 4 == 0 || (minf % 2 == 0 && xp_force)) &&
                  ((minf <= 64 && 2 * PB_WG / ((4096 + minf - 1) / minf + 1) >= 6) || xp_force) &&
@@ -1433,7 +1429,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         fe->land_pending = false;
     }
     pb_kargs K = S.K;
-    K.xcd_sh = (uint32_t)env_int("PBGPU_XCD_SH", 0); // (experiments) pb_xcd_region block size
+    K.xcd_rot = (uint32_t)env_int("PBGPU_XCD_ROT", 0); // (experiments) pb_xcd_region rotation
     K.first_iter = first_iter;
     K.n_frames = nf;
     K.out = out->data;
@@ -2051,6 +2047,9 @@ int pbgpu_kernel_times(pbgpu_ctx *ctx, double *ms_each, uint32_t cap, uint32_t *
     return PBGPU_OK;
 }
 
+static int fill_probe_buf(pbgpu_ctx *ctx, void *buf, uint64_t bytes, uint32_t reps, double *ms_per_shape,
+                          int *best_shape);
+
 int pbgpu_fill_probe_ex(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *ms_per_shape, int *best_shape)
 {
     if (ctx == NULL || bytes < 16 || reps == 0)
@@ -2059,6 +2058,23 @@ int pbgpu_fill_probe_ex(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *m
     PB_JOIN(ctx);
     void *buf = NULL;
     HIPCHK(hipMalloc(&buf, bytes));
+    const int rc = fill_probe_buf(ctx, buf, bytes, reps, ms_per_shape, best_shape);
+    (void)hipFree(buf);
+    return rc;
+}
+
+int pbgpu_fill_probe_at(pbgpu_ctx *ctx, void *dst, uint64_t bytes, uint32_t reps, double *ms_per_shape)
+{
+    if (ctx == NULL || dst == NULL || bytes < 16 || reps == 0)
+        return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
+    return fill_probe_buf(ctx, dst, bytes, reps, ms_per_shape, NULL);
+}
+
+static int fill_probe_buf(pbgpu_ctx *ctx, void *buf, uint64_t bytes, uint32_t reps, double *ms_per_shape,
+                          int *best_shape)
+{
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
@@ -2086,7 +2102,6 @@ int pbgpu_fill_probe_ex(pbgpu_ctx *ctx, uint64_t bytes, uint32_t reps, double *m
     }
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    (void)hipFree(buf);
     if (best_shape)
         *best_shape = bi;
     return PBGPU_OK;

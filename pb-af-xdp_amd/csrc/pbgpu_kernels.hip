@@ -328,23 +328,19 @@ constexpr uint32_t PB_C3 = PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u);
 // frames) taken by workgroup b: XCD x builds the x-th contiguous eighth of the regions, in
 // order, instead of every eighth region (the rest, fewer than 8, keep their own index).
 // Measured on the 1500-B staged kernel: 7.17 vs 8.45 ms per 2^25 frames.
-// sh > 0: XCD x takes blocks of G = 2^sh consecutive regions, block q * 8 + x for its q-th block,
-// so the eight XCDs' write fronts stay within one moving window of 8 G regions instead of eighths
-// of the launch apart (then the < G regions per XCD left over after the last full window: each
-// XCD's contiguous share of the tail, as sh = 0 does for the whole launch).
-__device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg, uint32_t sh = 0)
+// rot > 0 (experiments): XCD x starts its walk (x * rot * per / 256) regions into its eighth and
+// wraps, so the eight write fronts are per + rot * per / 256 regions apart instead of per.
+__device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg, uint32_t rot = 0)
 {
     const uint32_t per = nwg >> 3;
     if (b >= 8u * per)
         return b;
     const uint32_t x = b & 7u, j = b >> 3;
-    if (sh == 0)
+    if (rot == 0)
         return x * per + j;
-    const uint32_t full = (per >> sh) << sh; // regions per XCD in whole blocks
-    if (j < full)
-        return ((((j >> sh) << 3) + x) << sh) + (j & ((1u << sh) - 1u));
-    const uint32_t r = per - full;
-    return 8u * full + x * r + (j - full);
+    const uint32_t o = (uint32_t)(((uint64_t)per * rot * x) >> 8) % per;
+    const uint32_t jj = j + o;
+    return x * per + (jj >= per ? jj - per : jj);
 }
 
 // The reference's total_pckts / total_bytes (sequence.c:633-642), counted as work is done: each
@@ -650,7 +646,7 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
     __shared__ __attribute__((aligned(16))) uint32_t s_tile[WGT * NDW + 8];
 #endif
     const uint32_t tid = threadIdx.x;
-    const uint64_t f0 = (uint64_t)(PB_SMALL_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_sh) : blockIdx.x) * WGT;
+    const uint64_t f0 = (uint64_t)(PB_SMALL_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_rot) : blockIdx.x) * WGT;
     const uint64_t left = K.n_frames - f0;
     const uint32_t nfr = left < WGT ? (uint32_t)left : WGT;
     const uint32_t flen = K.fixed_len;
@@ -1545,7 +1541,7 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
     PB_STAMP(0);
     if (PB_TIMING)
         tt = __builtin_amdgcn_s_memtime();
-    const uint64_t f0 = (uint64_t)(PB_FST_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_sh) : blockIdx.x) * WF;
+    const uint64_t f0 = (uint64_t)(PB_FST_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_rot) : blockIdx.x) * WF;
     const uint64_t left = K.n_frames - f0;
     const uint32_t nfr = left < WF ? (uint32_t)left : WF;
     const uint64_t W0 = f0 * flen; // 16-B aligned
@@ -1759,7 +1755,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     uint32_t *const s_ord = s_win + CAP + 2; // frames of each window, longest first
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t bxr = PB_VST_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_sh) : blockIdx.x; // region
+    const uint32_t bxr = PB_VST_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_rot) : blockIdx.x; // region
     const uint32_t flags = K.flags;
     const uint32_t hl = K.hl;
     unsigned long long tt = 0; // PB_TIMING builds: phase stamps (slot 1 A, 3 windows + order, 2 B, 4 S)
@@ -2267,9 +2263,6 @@ static_assert(((PB_A3I * (PB_A3 & PB_M24)) & PB_M24) == 1u, "M^-1");
 #ifndef PB_ORB_LOG12
 #define PB_ORB_LOG12 1 // pb_orbit_sum: the discrete log's top 12 bits in closed form (0: 24 steps)
 #endif
-#ifndef PB_ORB_DOT4
-#define PB_ORB_DOT4 0 // pb_orbit_sum's walks: four bytes per v_dot4_u32_u8 pair (0: one byte per step)
-#endif
 #ifndef PB_ORB_BIDIR
 #define PB_ORB_BIDIR 1 // pb_orbit_sum walks to the nearer prefix-sum sample (<= 16 steps; 0: the next, <= 31)
 #endif
@@ -2337,31 +2330,6 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     uint32_t y = fp ? yp : __umul24(yp, PB_A3I) + PB_C3I; // backward: from position p - 1
     uint32_t z = fq ? yq : __umul24(yq, PB_A3I) + PB_C3I;
     uint32_t ap[2] = {0u, 0u}, aq[2] = {0u, 0u};
-    // (PBGPU_FST_DBG bit 7 flips PB_ORB_DOT4 at run time: a same-placement A/B, correct output)
-    if (PB_ORB_DOT4 ^ ((K.fst_dbg >> 7) & 1u))
-    {
-    // four walked bytes per step group: packed into one dword (bytes t = 4g .. 4g + 3), masked to
-    // the walk's length, summed by parity with two v_dot4_u32_u8 (13 instead of 20 VALU per group)
-    static_assert(HALF % 4 == 0, "walk groups");
-#pragma unroll
-    for (uint32_t g = 0; g < HALF / 4; ++g)
-    {
-        const uint32_t y1 = __umul24(y, ap_) + cp_, y2 = __umul24(y1, ap_) + cp_, y3 = __umul24(y2, ap_) + cp_;
-        const uint32_t z1 = __umul24(z, aq_) + cq_, z2 = __umul24(z1, aq_) + cq_, z3 = __umul24(z2, aq_) + cq_;
-        const uint32_t np = (uint32_t)min(max((int)dp - (int)(4 * g), 0), 4);
-        const uint32_t nq = (uint32_t)min(max((int)dq - (int)(4 * g), 0), 4);
-        const uint32_t bp = pb_pack4(y, y1, y2, y3) & (uint32_t)(0xFFFFFFFFull >> (32u - 8u * np));
-        const uint32_t bq = pb_pack4(z, z1, z2, z3) & (uint32_t)(0xFFFFFFFFull >> (32u - 8u * nq));
-        ap[0] = __builtin_amdgcn_udot4(bp, 0x00010001u, ap[0], false);
-        ap[1] = __builtin_amdgcn_udot4(bp, 0x01000100u, ap[1], false);
-        aq[0] = __builtin_amdgcn_udot4(bq, 0x00010001u, aq[0], false);
-        aq[1] = __builtin_amdgcn_udot4(bq, 0x01000100u, aq[1], false);
-        y = __umul24(y3, ap_) + cp_;
-        z = __umul24(z3, aq_) + cq_;
-    }
-    }
-    else
-    {
 #pragma unroll
     for (uint32_t t = 0; t < HALF; ++t)
     {
@@ -2369,7 +2337,6 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
         aq[t & 1u] += t < dq ? (z >> 16) & 0xFFu : 0u;
         y = __umul24(y, ap_) + cp_;
         z = __umul24(z, aq_) + cq_;
-    }
     }
     // even / odd position sums of the walked bytes (the first walked position: p, or p - 1)
     const uint32_t pp = fp ? p & 1u : (p & 1u) ^ 1u, pq = fq ? q & 1u : (q & 1u) ^ 1u;
@@ -2434,7 +2401,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     uint16_t *const s_map = reinterpret_cast<uint16_t *>(s_l48 + K.vl_nl48);
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t bxr = pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_sh); // XCD-contiguous regions
+    const uint32_t bxr = pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_rot); // XCD-contiguous regions
     const uint32_t flags = K.flags;
     const uint64_t f0 = (uint64_t)bxr * WF;
     const uint64_t left = K.n_frames - f0;
@@ -2493,8 +2460,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     for (int w = 0; w < 16; ++w)
         d[w] = 0u;
     uint32_t csum_v = 0; // PB_VL_LATE: the L4 checksum field, ORed into d[] after the scan
-    // (PBGPU_FST_DBG bit 8 flips PB_VL_LATE at run time: a same-placement A/B, correct output)
-    const bool vl_late = (PB_VL_LATE ^ ((K.fst_dbg >> 8) & 1u)) != 0;
+    constexpr bool vl_late = PB_VL_LATE != 0;
     if (valid)
     {
         uint64_t k;
@@ -3004,20 +2970,10 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
     }
     else if (K->xs_grid)
     {
-        const dim3 g(K->xs_grid);
-        const uint32_t w = NDW == 16 ? (K->xs_np << K->xs_fp_shift) : PB_WG; // 64 / 128 / 256 threads
-        if (K->pl0.random && w == 64)
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true, 64>), g, dim3(64), K->lds_pad, st, *K);
-        else if (K->pl0.random && w == 128)
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true, 128>), g, dim3(128), K->lds_pad, st, *K);
-        else if (K->pl0.random)
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), g, dim3(PB_WG), K->lds_pad, st, *K);
-        else if (w == 64)
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false, 64>), g, dim3(64), K->lds_pad, st, *K);
-        else if (w == 128)
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false, 128>), g, dim3(128), K->lds_pad, st, *K);
+        if (K->pl0.random)
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, true>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
         else
-            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false>), g, dim3(PB_WG), K->lds_pad, st, *K);
+            hipLaunchKernelGGL((pb_xsmall_kernel<NDW, PROTO, false>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
     }
     else if (K->fixed_len % 4 == 2) // 98-B ICMP, 106-B UDP: only the 2-mod-4 tile writes compiled in
     {

@@ -287,6 +287,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pbgpu_kernel_times": (C.c_int, [P, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint32)]),
         "pbgpu_fill_probe": (C.c_int, [P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
         "pbgpu_fill_probe_ex": (C.c_int, [P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+        "pbgpu_fill_probe_at": (C.c_int, [P, C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
         "pbgpu_fill_shape_name": (C.c_char_p, [C.c_int]),
         "pbgpu_abi_size": (C.c_size_t, [C.c_int]),
         "pbgpu_kernel_name": (C.c_int, [P, C.c_uint16, C.c_char_p, C.c_size_t]),
@@ -450,6 +451,13 @@ class GpuContext:
         _check(self.lib.pbgpu_fill_probe_ex(self.h, nbytes, reps, ms, C.byref(best)), "fill_probe_ex")
         names = [self.lib.pbgpu_fill_shape_name(i).decode() for i in range(self.FILL_SHAPES)]
         return {names[i]: float(ms[i]) for i in range(self.FILL_SHAPES)}, names[best.value]
+
+    def fill_probe_at(self, fb: "FrameBuffer", nbytes: int, reps: int):
+        """Every write-probe shape's mean ms per launch over a frame buffer's own memory."""
+        ms = (C.c_double * self.FILL_SHAPES)()
+        _check(self.lib.pbgpu_fill_probe_at(self.h, fb.f.data, nbytes, reps, ms), "fill_probe_at")
+        names = [self.lib.pbgpu_fill_shape_name(i).decode() for i in range(self.FILL_SHAPES)]
+        return {names[i]: float(ms[i]) for i in range(self.FILL_SHAPES)}
 
     def kernel_name(self, idx: int) -> str:
         buf = C.create_string_buffer(96)

@@ -25,12 +25,17 @@ for d in sorted(glob.glob(os.path.join(out_dir, "pmc_*"))):
             kn = r["Kernel_Name"]
             build = kn.startswith("void pb_") and any(x in kn for x in ("gpf", "stage", "small", "xpage", "vline"))
             aux = kn.startswith("void pb_len_") or kn.startswith("pb_len_") or "pb_scan_blocks" in kn
+            fold = "pb_ctr_fold" in kn  # the counters' fold: its bytes spread over the build launches
+            aux = aux or fold
             if not (build or aux):
                 continue
             agg[(kn, r["Counter_Name"], aux)].append(float(r["Counter_Value"]))
+        builds = {cn: len(v) for (kn, cn, aux), v in agg.items() if not aux}
         for (kn, cn, aux), v in agg.items():
             e = res["per_launch"].setdefault(cfg, {"kernel": None, "aux": {}})
-            if aux:  # the length scan of variable-length frames: part of each step's traffic
+            if aux and "pb_ctr_fold" in kn:  # amortized: its total over the run's build launches
+                e["aux"].setdefault(kn, {})[cn] = sum(v) / max(1, builds.get(cn, len(v)))
+            elif aux:  # the length scan of variable-length frames: part of each step's traffic
                 e["aux"].setdefault(kn, {})[cn] = sum(v) / len(v)
             else:
                 e["kernel"] = kn

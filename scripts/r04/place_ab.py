@@ -42,6 +42,15 @@ for rnd in range(int(os.environ.get("ROUNDS", "2"))):
             ms, cnt = ctx.kernel_time()
             res.setdefault((tag, i), []).append(ms / cnt)
 addr = [hex(C.cast(fb.ptr.contents.data, C.c_void_p).value or 0) for fb in bufs]
+if os.environ.get("FILL"):  # the plain fill shapes over each buffer's own memory (GB/s)
+    for key in keys:
+        os.environ.pop(key, None)
+    nb = (bufs[0].f.capacity_bytes // 65536) * 65536
+    for i, fb in enumerate(bufs):
+        shapes = ctx.fill_probe_at(fb, nb, 5)
+        print(json.dumps({"config": cfg, "buf": i, "addr": addr[i], "fill_gbps": {k: round(nb / (v * 1e-3) / 1e9, 1)
+                                                                                  for k, v in shapes.items()}}),
+              flush=True)
 for tag, _ in variants:
     per = [round(min(res[(tag, i)]), 4) for i in range(nbuf)]
     print(json.dumps({"config": cfg, "tag": tag, "kernel": ctx.kernel_name(0), "ms_min_per_buffer": per,

@@ -148,15 +148,12 @@ XS_LENS = [42, 43, 44, 48, 52, 56, 60, 64, 72, 96, 98, 100, 106, 108, 116, 120, 
 XS_COUNTS = [1, 5, 200, 2048, 2049, 2 * 2048 * 5 + 77]
 
 
-@pytest.mark.parametrize("force_xpage", [False, True, 512, "lin64", "lin128", "fa64", "xs64", "xs128"],
+@pytest.mark.parametrize("force_xpage", [False, True, 512, "lin64", "lin128", "fa64"],
                          ids=["default", "xpage_forced", "xpage_forced_512", "linear_wg64", "linear_wg128",
-                              "xpage_forced_fa64", "xsmall_wg64", "xsmall_wg128"])
+                              "xpage_forced_fa64"])
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
 @pytest.mark.parametrize("flen", XS_LENS)
 def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
-    if force_xpage in ("xs64", "xs128"):  # pb_xsmall_kernel with one / two pages per workgroup
-        monkeypatch.setenv("PBGPU_XS_WGT", force_xpage[2:])
-        force_xpage = False
     if force_xpage == "fa64":  # pb_xpage_kernel's 64-bit first-frame path at every size
         monkeypatch.setenv("PBGPU_XP_FA64", "1")
     if force_xpage:
