@@ -168,6 +168,7 @@ struct pb_kargs
     // sequences, {frames, bytes} for variable ones, at position pb_xcd_region(blockIdx.x); the
     // host folds them into `counters` (pb_ctr_fold).  Null: one atomic per workgroup instead.
     uint32_t *ctr_slots;
+    uint32_t store_flip;    // (experiments, PBGPU_STORE_FLIP=1) pb_vline_kernel / pb_small_kernel: the other store kind
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

@@ -1243,7 +1243,9 @@ int pbgpu_frames_alloc(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capaci
         return PBGPU_ENOMEM;
     capacity_bytes = (capacity_bytes + 15) & ~15ull;
     // +64 B: word-granular readers (UMEM scatter) may touch a few bytes past the last frame
-    if (hipMalloc((void **)&f->data, capacity_bytes + 64) != hipSuccess ||
+    // (experiments) PBGPU_ALLOC_CONTIG=1: physically contiguous frame memory
+    const unsigned alloc_flags = env_is("PBGPU_ALLOC_CONTIG", "1") ? hipDeviceMallocContiguous : hipDeviceMallocDefault;
+    if (hipExtMallocWithFlags((void **)&f->data, capacity_bytes + 64, alloc_flags) != hipSuccess ||
         hipMalloc((void **)&f->offsets, (capacity_frames + 1) * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc((void **)&f->scan_tmp, scan_tmp_bytes(capacity_frames)) != hipSuccess)
     {
@@ -1430,6 +1432,7 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     }
     pb_kargs K = S.K;
     K.xcd_rot = (uint32_t)env_int("PBGPU_XCD_ROT", 0); // (experiments) pb_xcd_region rotation
+    K.store_flip = env_is("PBGPU_STORE_FLIP", "1") ? 1u : 0u;
     K.first_iter = first_iter;
     K.n_frames = nf;
     K.out = out->data;
@@ -1525,7 +1528,10 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
                     (void)hipFree(S.d_ctr_slots);
                 S.d_ctr_slots = nullptr;
                 S.ctr_cap = 0;
-                const uint64_t cap = words > PB_CTR_RING_WORDS ? words : PB_CTR_RING_WORDS;
+                // (PBGPU_CTR_RING = words: a small ring, so the tests reach the fold-when-full path)
+                const int er = env_int("PBGPU_CTR_RING", 0);
+                const uint64_t ring = er > 0 ? (uint64_t)er : PB_CTR_RING_WORDS;
+                const uint64_t cap = words > ring ? words : ring;
                 HIPCHK(hipMalloc((void **)&S.d_ctr_slots, cap * sizeof(uint32_t)));
                 S.ctr_cap = cap;
             }
@@ -2144,7 +2150,8 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_xpage_kernel<%u, %u, %s, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
                  K.xp_wgt, K.fixed_len % 4 == 0 ? "true" : "false");
     else if (K.xs_np && !env_is("PBGPU_KERNEL", "linear"))
-        snprintf(buf, n, "pb_xsmall_kernel<%u, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false");
+        snprintf(buf, n, "pb_xsmall_kernel<%u, %u, %s, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
+                 (uint32_t)PB_WG);
     else
         snprintf(buf, n, "pb_small_kernel<%u, %u, %s, %u, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
                  K.small_wgt ? K.small_wgt : (uint32_t)PB_WG, K.fixed_len % 4 == 2 ? 2u : 0u);

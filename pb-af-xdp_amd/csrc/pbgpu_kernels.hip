@@ -202,6 +202,15 @@ __device__ __forceinline__ void pb_st16_sx(uint8_t *p, pb_u32x4 v)
 #ifndef PB_VL_NT
 #define PB_VL_NT 1 // pb_vline_kernel's frame stores are non-temporal
 #endif
+// NT: the store kind as a template parameter (each kernel instance keeps one kind)
+template <bool NT>
+__device__ __forceinline__ void pb_st16_k(uint8_t *p, pb_u32x4 v)
+{
+    if (NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
+    else
+        *reinterpret_cast<pb_u32x4 *>(p) = v;
+}
 __device__ __forceinline__ void pb_st16_vl(uint8_t *p, pb_u32x4 v)
 {
 #if PB_VL_NT
@@ -637,7 +646,7 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
 // Linear form: workgroup b builds frames [WGT b, WGT b + WGT) and writes their
 // contiguous byte range (WGT = 256, or 128 / 64: smaller regions per workgroup).  Used when the output is not 4 KiB aligned (and under
 // PBGPU_KERNEL=linear for comparison).
-template <int NDW, int PROTO, bool RANDOM, int WGT, int AL = 0> // AL: pb_small_put's alignment class
+template <int NDW, int PROTO, bool RANDOM, int WGT, int AL = 0, bool NT = PB_SX_NT != 0> // AL: pb_small_put's alignment class
 __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
 {
 #if PB_SMALL_DYN
@@ -673,7 +682,7 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
             for (int t = 0; t < 4; ++t)
                 v[t] &= pb_range_mask(0, (int)tile_bytes - (int)(16 * c + 4 * t));
         }
-        pb_st16_sx(out + 16 * c, v);
+        pb_st16_k<NT>(out + 16 * c, v);
     }
     if (tid == 0)
         pb_count(K, blockIdx.x, nfr, tile_bytes);
@@ -2383,7 +2392,7 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
 #ifndef PB_VL_IMGW
 #define PB_VL_IMGW 1 // prologue: header images as NHW dword writes, line map as plain writes + the last line
 #endif
-template <int HL, bool L4>
+template <int HL, bool L4, bool NT = PB_VL_NT != 0> // NT: non-temporal frame stores
 __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
 {
     constexpr uint32_t GH = PB_VST_GHOSTS;
@@ -2435,7 +2444,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             {
                 const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
                 if (c0 < R)
-                    pb_st16_vl(K.out + lo + c0, pb_u32x4{c0, s, i, (uint32_t)lo});
+                    pb_st16_k<NT>(K.out + lo + c0, pb_u32x4{c0, s, i, (uint32_t)lo});
             }
         return;
     }
@@ -2671,7 +2680,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             {
                 const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
                 if (c0 < R)
-                    pb_st16_vl(gout + c0, pb_u32x4{c0, s, i, lo_rel});
+                    pb_st16_k<NT>(gout + c0, pb_u32x4{c0, s, i, lo_rel});
             }
     const uint32_t k = lane & 7u, kk = k | (k << 4), ck = (lo_rel >> 4) + k;
     const uint32_t lmax = nlines ? nlines - 1u : 0u;
@@ -2714,7 +2723,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             v[i] = chunk(s, i, false);
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
-            pb_st16_vl(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
+            pb_st16_k<NT>(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
     }
     for (uint32_t s = nfull; s < nsteps; ++s)
     {
@@ -2728,7 +2737,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         {
             const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
             if (store && c0 < R)
-                pb_st16_vl(gout + c0, v[i]);
+                pb_st16_k<NT>(gout + c0, v[i]);
         }
     }
     if (tid == 0) // the workgroup stores exactly [lo, hi) (the launch's last chunk zero-padded)
@@ -2929,7 +2938,10 @@ static void pbk_launch_linear(const pb_kargs *K, hipStream_t st)
     const uint32_t wgt = K->small_wgt ? K->small_wgt : PB_WG;
     const dim3 g((uint32_t)((K->n_frames + wgt - 1) / wgt));
     const size_t lds = pb_small_tile_bytes(wgt, K->fixed_len) + K->lds_pad;
-    if (wgt == 64)
+    constexpr bool NT = PB_SX_NT != 0;
+    if (K->store_flip && wgt == 64) // (experiments) the other store kind
+        hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, RANDOM, 64, AL, !NT>), g, dim3(64), lds, st, *K);
+    else if (wgt == 64)
         hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, RANDOM, 64, AL>), g, dim3(64), lds, st, *K);
     else if (wgt == 128)
         hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, RANDOM, 128, AL>), g, dim3(128), lds, st, *K);
@@ -3026,6 +3038,7 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
         const uint32_t grid = (uint32_t)((K->n_frames + K->vl_wgf - 1) / K->vl_wgf);
         const size_t lds = PB_VL_LDS(K->vl_wgf, K->hl == 54 ? 5 : 4, K->vl_nl48, K->vl_nlines) + K->lds_pad;
         const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
+        constexpr bool NT = PB_VL_NT != 0;
         if (K->hl == 54)
         {
             if (l4)
@@ -3033,6 +3046,8 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
             else
                 hipLaunchKernelGGL((pb_vline_kernel<54, false>), dim3(grid), dim3(PB_WG), lds, st, *K);
         }
+        else if (K->store_flip && l4) // (experiments) the other store kind
+            hipLaunchKernelGGL((pb_vline_kernel<42, true, !NT>), dim3(grid), dim3(PB_WG), lds, st, *K);
         else
         {
             if (l4)
