@@ -21,7 +21,8 @@ for v in sys.argv[5:]:
     variants.append((tag, dict(e.split("=", 1) for e in envs.split(",") if e)))
 keys = {key for _, e in variants for key in e}
 ctx = GpuContext(0)
-ctx.load_sequence(0, Sequence.from_config(pc.get(cfg)), pc.SEED_BASE)
+seq = Sequence.from_config(pc.get(cfg))
+ctx.load_sequence(0, seq, pc.SEED_BASE)
 ctx.set_timing(ctx.TIMING_SPAN)
 bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(nbuf)]
 t0 = time.perf_counter()
@@ -36,6 +37,7 @@ for rnd in range(int(os.environ.get("ROUNDS", "2"))):
             for key in keys:
                 os.environ.pop(key, None)
             os.environ.update(env)
+            ctx.load_sequence(0, seq, pc.SEED_BASE)  # load-time switches (PBGPU_FST_DBG) take effect
             for s in range(k):
                 ctx.build(0, s * n, n, fb)
             ctx.sync()
@@ -45,7 +47,9 @@ addr = [hex(C.cast(fb.ptr.contents.data, C.c_void_p).value or 0) for fb in bufs]
 if os.environ.get("FILL"):  # the plain fill shapes over each buffer's own memory (GB/s)
     for key in keys:
         os.environ.pop(key, None)
-    nb = (bufs[0].f.capacity_bytes // 65536) * 65536
+    # the bytes one build writes (configs[2] writes ~27.6 of its 51.7-GB capacity)
+    nb = (min(fb.total_bytes() for fb in bufs) // 65536) * 65536 if not os.environ.get("FILL_CAP") else \
+        (bufs[0].f.capacity_bytes // 65536) * 65536
     for i, fb in enumerate(bufs):
         shapes = ctx.fill_probe_at(fb, nb, 5)
         print(json.dumps({"config": cfg, "buf": i, "addr": addr[i], "fill_gbps": {k: round(nb / (v * 1e-3) / 1e9, 1)
