@@ -943,25 +943,28 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 ++K.xs_fp_shift;
             K.xs_np = 256 >> K.xs_fp_shift;
         }
-        else if ((minf % 4 == 0 || (minf % 2 == 0 && xp_force)) &&
-                 ((minf <= 64 && 2 * PB_WG / ((4096 + minf - 1) / minf + 1) >= 6) || xp_force) &&
-                 !env_is("PBGPU_KERNEL", "nopage"))
+        else if ((xp_force && minf % 2 == 0) ||
+                 (!env_is("PBGPU_KERNEL", "nopage") && minf % 2 == 0 && minf >= 52 && minf <= 128 &&
+                  (minf % 4 == 0 && minf <= 64 ? true : !pls[0].random && !env_is("PBGPU_XP_STATIC", "0"))))
         {
-            // pages of frames cut at the page edges (pb_xpage_kernel): one slot per frame
-            // touching a page; pages per workgroup = the slots of two passes of 256 lanes,
-            // at most 7 (30 KiB of LDS, 5 workgroups per CU).  60-B TCP SYN, 2^25 frames
-            // (profiles/r01/xpage): 7 pages 0.318-0.336 ms, 4 / 3 / 2 pages 0.387 / 0.405 /
-            // 0.50, 10 / 14 pages 0.374 / 0.458; the linear small kernel 0.353-0.372.  Taken
-            // for frames <= 64 B whose workgroup gets >= 6 pages (52-64 B): by length
-            // (len_ab.txt) it wins 4-12% there for UDP and TCP, loses 5-12% at 44-48 B (5
-            // pages) and 12-20% over 64 B, where the 32-dword frame spills kernel-argument
-            // SGPRs (PBGPU_XP_FORCE=1 takes it for any length % 4 == 0).
+            // XCD-owned 4 KiB pages for frames cut at the page edges (pb_xpage_kernel): one slot
+            // per frame touching a page, 512-thread workgroups (one pass of slots): lengths of
+            // 52-64 B that are multiples of 4, and static payloads at every even length of 52-128 B
+            // that does not divide 4096.  Round 4 (profiles/r04/ab/len_*.jsonl, xp_*.jsonl): static
+            // payloads 5-16% faster than the linear small kernel at 54-126 B, 13% at the 98-B ICMP
+            // frame (0.474-0.481 vs 0.549-0.552 ms, 4 buffers), and the rate does not depend on the
+            // buffer's placement; random payloads over 64 B or of 2 mod 4 lose
+            // 20-30% (each straddling frame's payload generated twice); 60-B TCP 512 vs 256
+            // threads 0.296-0.298 vs 0.300-0.302 ms.  Pages per workgroup: 9 for lengths of 2 mod 4 (98 B:
+            // 0.474-0.481 ms vs 0.496-0.501 at 7, 0.489-0.491 at 11, 0.574-0.577 at 5), 7 otherwise
+            // (68 / 100 / 120 B: 7 faster than 9), at most the slots of one pass.
             K.xp = 1;
             K.xp_fpp = (4096 + minf - 1) / minf + 1;
             K.xp_div = make_div(K.xp_fpp);
             K.xp_inv = 1.0 / (double)minf;
-            K.xs_np = std::max<uint32_t>(1, std::min<uint32_t>(7, 2 * PB_WG / K.xp_fpp));
-            K.xp_wgt = (uint32_t)env_int("PBGPU_XP_WGT", 256) == 512 ? 512 : 256;
+            K.xp_wgt = (uint32_t)env_int("PBGPU_XP_WGT", 512) == 256 ? 256 : 512;
+            const uint32_t want = minf % 4 == 2 ? 9u : 7u;
+            K.xs_np = std::max<uint32_t>(1, std::min<uint32_t>(want, 2 * PB_WG / K.xp_fpp));
             const int enp = env_int("PBGPU_XP_NP", 0); // at most two frame slots per 256 lanes
             if (enp > 0 && (uint32_t)enp * K.xp_fpp <= 2 * PB_WG)
                 K.xs_np = (uint32_t)enp;

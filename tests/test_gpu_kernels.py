@@ -160,6 +160,8 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
         monkeypatch.setenv("PBGPU_XP_FORCE", "1")
     if force_xpage == 512:
         monkeypatch.setenv("PBGPU_XP_WGT", "512")
+    elif force_xpage is True:  # the 256-thread form (two passes of slots per lane)
+        monkeypatch.setenv("PBGPU_XP_WGT", "256")
     lin = force_xpage in ("lin64", "lin128")
     if lin:  # the linear small kernel at 64 / 128 frames per workgroup, for every length
         monkeypatch.delenv("PBGPU_XP_FORCE", raising=False)
@@ -176,10 +178,11 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
     for n in XS_COUNTS:
         n = max(1, n * 64 // flen)  # page counts as named above at every length
         kern = _check(ctx, cfg, 1000003 + n, n)
-        xp_default = flen <= 64 and 512 // ((4096 + flen - 1) // flen + 1) >= 6
+        # pbgpu_load_sequence: 52-64 B multiples of 4; static payloads at even 52-128 B
+        xp_default = 52 <= flen <= 64 and flen % 4 == 0 or (proto == "icmp" and 52 <= flen <= 128)
         if lin:
             want = "pb_small_kernel<"
-        elif (flen % 4 == 0 or (force_xpage and flen % 2 == 0)) and (force_xpage or (4096 % flen and xp_default)):
+        elif flen % 2 == 0 and (force_xpage or (4096 % flen and xp_default)):
             want = "pb_xpage_kernel"
         else:
             want = "pb_xsmall_kernel" if 4096 % flen == 0 else "pb_small_kernel<"
