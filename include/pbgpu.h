@@ -142,9 +142,10 @@ int pbgpu_host_register(pbgpu_ctx *ctx, void *ptr, size_t bytes);
 int pbgpu_host_unregister(pbgpu_ctx *ctx, void *ptr);
 
 /* ---- counters (sequence.c:12-14, 633-642): frames built / bytes stored per
- * sequence since open, added by the build kernels' workgroups as they finish
- * their share (a skipped or short build shows here); multi-GPU callers
- * all-reduce these over RCCL. ---- */
+ * sequence since open, recorded by the build kernels' workgroups as they finish
+ * their share (a skipped or short build shows here) and folded into the totals
+ * here, when a sequence's record ring fills and when its slot is reloaded;
+ * multi-GPU callers all-reduce these over RCCL. ---- */
 int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq);
 
 /* ---- measurement ---- */
