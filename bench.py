@@ -123,7 +123,14 @@ def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ram
     ctx.set_timing(ctx.TIMING_SPAN)
     step_iter = lambda s: pb_dist.step_first_iter(s, rank, world, n_pkts)  # noqa: E731
 
+    # several sequences: one pbgpu_build_batch call per step (configs[4]'s three: one fused
+    # launch, pb_batch_kernel; PBGPU_BATCH=0: one launch per sequence on its own stream)
+    batch = nseq > 1 and os.environ.get("PBGPU_BATCH", "1") != "0"
+
     def step(s):
+        if batch:
+            ctx.build_batch([(i, step_iter(s), n_pkts, bufs[i]) for i in range(nseq)])
+            return
         for i in range(nseq):
             ctx.build(i, step_iter(s), n_pkts, bufs[i])
 
@@ -162,6 +169,7 @@ def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ram
     barrier(dist, local)
     wall = time.perf_counter() - t0
     k_ms, k_n = ctx.kernel_time()
+    per_step_launches = max(1, k_n // steps)
     # a separate pass with an event pair around every launch: each launch's own device
     # time (median / min / max; the pairs add ~10 us between launches, so `value` and
     # the roofline come from the span above, not from this pass)
@@ -174,12 +182,15 @@ def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ram
         t = ctx.kernel_times()
         ctx.set_timing(ctx.TIMING_SPAN)
         if len(t):
-            per_step = t.reshape(-1, nseq).sum(axis=1) if len(t) % nseq == 0 else t
+            per_step = t.reshape(-1, per_step_launches).sum(axis=1) if len(t) % per_step_launches == 0 else t
             per_launch = {"median": round(float(np.median(per_step)), 5), "min": round(float(per_step.min()), 5),
                           "max": round(float(per_step.max()), 5), "n": int(len(per_step)),
                           "mode": "HIP event pair around every launch, separate pass after the timed span"}
     flens = [int(fb.f.fixed_len) for fb in bufs]
     kernels = [ctx.kernel_name(i) for i in range(nseq)]
+    if nseq > 1 and per_step_launches == 1:  # the fused launch, running each sequence's kernel body
+        wgt = 256 if os.environ.get("PBGPU_BATCH_WGT") == "256" else 512
+        kernels = [f"pb_batch_kernel<{wgt}, 1, 2, 3>"] + [f"(part) {k}" for k in kernels]
     for fb in bufs:
         fb.free()
     if dist is not None:
@@ -341,6 +352,9 @@ def main():
     if rank != 0:
         return
     doc = " ".join((pc.c5_mix if a.config == "c5_mix" else pc.BASELINE[a.config]).__doc__.split())
+    # the fused mix launch's own PMC pass when the summary has one (else the parts' passes summed)
+    mix_traffic = pmc_traffic(a.pmc, ["c5_mix"], a.packets) if a.config == "c5_mix" and \
+        res["kernels"][0].startswith("pb_batch_kernel") else None
     line = {
         "metric": "device-resident Mpps & GB/s, 64B and 1500B UDP, L3+L4 checksums on",
         "value": round(mpps, 3),
@@ -366,7 +380,8 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "frac_of_guide_achievable": round(achieved / HBM_ACHIEVABLE_GBPS, 4),
                      "frac_of_measured_write_peak": round(achieved / peak_probe, 4) if peak_probe else None,
-                     "traffic": pmc_traffic(a.pmc, names, a.packets), "traffic_source": os.path.relpath(a.pmc, ROOT),
+                     "traffic": mix_traffic if mix_traffic is not None else pmc_traffic(a.pmc, names, a.packets),
+                     "traffic_source": os.path.relpath(a.pmc, ROOT),
                      "kernel": res["kernels"][0] if len(names) == 1 else res["kernels"],
                      "kernel_ms_avg": round(res["span_ms_per_step"], 5),
                      "per_launch_ms": res["per_launch_ms"],

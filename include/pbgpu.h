@@ -108,6 +108,17 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *frames);
 int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter,
                 pbgpu_frames *out);
 
+/* Several sequences' builds at once: part i builds iterations [first_iter[i],
+ * first_iter[i] + n_iter[i]) of sequence seq_idx[i] into outs[i], exactly as
+ * pbgpu_build() would (same frames, offsets and counters).  The reference runs
+ * its sequences side by side (sequence.c:741-762, one thread group per
+ * sequence); configs[4]'s three (64-B UDP, 60-B TCP SYN, 98-B ICMP echo, each
+ * into its own 4-KiB-aligned buffer) are built by one fused launch
+ * (pb_batch_kernel), any other set by one launch per part.  PBGPU_BATCH=0:
+ * always one launch per part. */
+int pbgpu_build_batch(pbgpu_ctx *ctx, uint32_t n, const uint16_t *seq_idx, const uint64_t *first_iter,
+                      const uint64_t *n_iter, pbgpu_frames *const *outs);
+
 int pbgpu_sync(pbgpu_ctx *ctx);
 int pbgpu_frames_total(pbgpu_ctx *ctx, pbgpu_frames *frames, uint64_t *total_bytes);
 /* Fills offsets[0 .. n_frames) of a variable-length build (ordered on the context's

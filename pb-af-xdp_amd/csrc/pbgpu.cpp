@@ -28,6 +28,8 @@
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st);
 extern "C" uint32_t pbk_build_grid(const pb_kargs *K);
+extern "C" int pbk_batch_kind(const pb_kargs *K);
+extern "C" hipError_t pbk_launch_batch(const pb_kargs *Ks, uint32_t wgt, hipStream_t st);
 extern "C" hipError_t pbk_launch_ctr_fold(const uint32_t *slots, uint64_t n, uint32_t pairs,
                                           unsigned long long *counters, hipStream_t st);
 extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
@@ -1385,7 +1387,19 @@ int pbgpu_frames_offsets(pbgpu_ctx *ctx, pbgpu_frames *f)
     return materialize_offsets(ctx, f);
 }
 
-int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, pbgpu_frames *out)
+// A part of pbgpu_build_batch's fused launch: the stream it runs on and its block size in; the
+// build's kargs out (built = false: no frames, nothing to launch)
+struct batch_part
+{
+    hipStream_t st;
+    uint32_t wgt;
+    pb_kargs K;
+    bool built;
+};
+
+// pbgpu_build, or with bp: every step of it but the launch (and its timing), on bp->st
+static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, pbgpu_frames *out,
+                      batch_part *bp)
 {
     if (ctx == NULL || out == NULL || seq_idx >= PB_MAX_SEQUENCES)
         return PBGPU_EINVAL;
@@ -1407,7 +1421,9 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     hipStream_t st = ctx->stream;
     const bool span = ctx->timing_mode == PBGPU_TIMING_SPAN;
     int si = -1;
-    if (span && !env_is("PBGPU_SEQ_STREAMS", "0"))
+    if (bp)
+        st = bp->st, bp->built = false;
+    else if (span && !env_is("PBGPU_SEQ_STREAMS", "0"))
     {
         si = seq_idx % PB_SEQ_STREAMS;
         if (ctx->seq_stream[si] == nullptr)
@@ -1496,6 +1512,8 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         }
     }
     K.xs_grid = 0;
+    if (bp && K.small_ndw && K.xs_np && !K.xp) // pb_xsmall_body at the batch's block size
+        K.xs_np = bp->wgt >> K.xs_fp_shift;
     if (K.small_ndw && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && !env_is("PBGPU_KERNEL", "linear"))
     {
         // XCD-owned 4 KiB pages (pb_xsmall_kernel): groups of 8 workgroups x 4 pages, tail pages in order
@@ -1543,6 +1561,12 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
             return rc;
         K.ctr_slots = S.d_ctr_slots + S.ctr_used;
         S.ctr_used += words;
+    }
+    if (bp)
+    {
+        bp->K = K;
+        bp->built = true;
+        return PBGPU_OK;
     }
     timing_pair tp = {nullptr, nullptr};
     if (!span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
@@ -1603,6 +1627,114 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
         uint32_t n;
         rc = pbgpu_kernel_time(ctx, &ms, &n);
         if (rc)
+            return rc;
+    }
+    return PBGPU_OK;
+}
+
+int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, pbgpu_frames *out)
+{
+    return build_impl(ctx, seq_idx, first_iter, n_iter, out, nullptr);
+}
+
+// pb_batch_kernel's block size (PBGPU_BATCH_WGT=256: the 256-thread form)
+static uint32_t batch_wgt()
+{
+    return env_int("PBGPU_BATCH_WGT", 512) == 256 ? 256u : 512u;
+}
+
+// The fused form applies: three distinct sequences of kinds 1, 2, 3 (pbk_batch_kind), into three
+// distinct 4-KiB-aligned buffers, each with frames to build; order[k] = the part of kind k + 1
+static bool batch_fusable(pbgpu_ctx *ctx, uint32_t n, const uint16_t *seq_idx, const uint64_t *n_iter,
+                          pbgpu_frames *const *outs, uint32_t order[3])
+{
+    if (n != 3 || env_is("PBGPU_BATCH", "0") || env_is("PBGPU_KERNEL", "linear"))
+        return false;
+    bool seen[3] = {false, false, false};
+    for (uint32_t i = 0; i < 3; ++i)
+    {
+        const seq_slot &S = ctx->seqs[seq_idx[i]];
+        const int kd = S.loaded ? pbk_batch_kind(&S.K) : 0;
+        if (kd < 1 || kd > 3 || seen[kd - 1] || n_iter[i] == 0 || ((uintptr_t)outs[i]->data & 4095u) != 0)
+            return false;
+        seen[kd - 1] = true;
+        order[kd - 1] = i;
+        for (uint32_t j = 0; j < i; ++j)
+            if (seq_idx[j] == seq_idx[i] || outs[j] == outs[i])
+                return false;
+    }
+    return true;
+}
+
+int pbgpu_build_batch(pbgpu_ctx *ctx, uint32_t n, const uint16_t *seq_idx, const uint64_t *first_iter,
+                      const uint64_t *n_iter, pbgpu_frames *const *outs)
+{
+    if (ctx == NULL || (n && (seq_idx == NULL || first_iter == NULL || n_iter == NULL || outs == NULL)))
+        return PBGPU_EINVAL;
+    for (uint32_t i = 0; i < n; ++i)
+        if (outs[i] == NULL || seq_idx[i] >= PB_MAX_SEQUENCES)
+            return PBGPU_EINVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    uint32_t order[3];
+    if (!batch_fusable(ctx, n, seq_idx, n_iter, outs, order))
+    {
+        // no fused form: one launch per part, as pbgpu_build
+        for (uint32_t i = 0; i < n; ++i)
+        {
+            const int rc = pbgpu_build(ctx, seq_idx[i], first_iter[i], n_iter[i], outs[i]);
+            if (rc != PBGPU_OK)
+                return rc;
+        }
+        return PBGPU_OK;
+    }
+    // every part on the context's stream, then one launch
+    hipStream_t st = ctx->stream;
+    const bool span = ctx->timing_mode == PBGPU_TIMING_SPAN;
+    batch_part bp[3]; // (build_impl orders each part after its buffer's and count ring's last stream)
+    pb_kargs Ks[3];
+    for (uint32_t k = 0; k < 3; ++k)
+    {
+        const uint32_t i = order[k];
+        bp[k].st = st;
+        bp[k].wgt = batch_wgt();
+        const int rc = build_impl(ctx, seq_idx[i], first_iter[i], n_iter[i], outs[i], &bp[k]);
+        if (rc != PBGPU_OK)
+            return rc;
+        if (!bp[k].built)
+            return PBGPU_EINVAL; // (n_iter > 0 was checked: unreachable)
+        Ks[k] = bp[k].K;
+    }
+    if (span)
+    {
+        if (ctx->span_n == 0)
+        {
+            if (ctx->span.a == nullptr)
+            {
+                HIPCHK(hipEventCreate(&ctx->span.a));
+                HIPCHK(hipEventCreate(&ctx->span.b));
+            }
+            HIPCHK(hipEventRecord(ctx->span.a, ctx->stream));
+            for (bool &j : ctx->seq_in_span)
+                j = false;
+        }
+        HIPCHK(pbk_launch_batch(Ks, batch_wgt(), st));
+        ++ctx->span_n;
+    }
+    else
+    {
+        timing_pair tp = {nullptr, nullptr};
+        int rc = timed_pair(ctx, &tp);
+        if (rc != PBGPU_OK)
+            return rc;
+        HIPCHK(hipEventRecord(tp.a, st));
+        HIPCHK(pbk_launch_batch(Ks, batch_wgt(), st));
+        HIPCHK(hipEventRecord(tp.b, st));
+        ctx->pending.push_back(tp);
+    }
+    for (uint32_t i = 0; i < 3; ++i)
+    {
+        const int rc = mark_built(ctx, outs[i], st);
+        if (rc != PBGPU_OK)
             return rc;
     }
     return PBGPU_OK;

@@ -364,13 +364,14 @@ __device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg, uint
 #ifndef PB_COUNT
 #define PB_COUNT 1 // (A/B builds) 0: no counting at all (wrong counters; measures its cost)
 #endif
-__device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t frames, uint64_t bytes)
+// (pos: the record's index in the launch's slot array; pb_batch_kernel passes the part's own)
+__device__ __forceinline__ void pb_count_at(const pb_kargs &K, uint32_t b, uint32_t pos, uint64_t frames,
+                                            uint64_t bytes)
 {
     if (!PB_COUNT)
         return;
     if (K.ctr_slots)
     {
-        const uint32_t pos = pb_xcd_region(blockIdx.x, gridDim.x);
         if (K.fixed_len)
             K.ctr_slots[pos] = (uint32_t)bytes;
         else
@@ -381,6 +382,10 @@ __device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t
     if (!K.fixed_len)
         atomicAdd(c, (unsigned long long)frames);
     atomicAdd(c + 1, (unsigned long long)bytes);
+}
+__device__ __forceinline__ void pb_count(const pb_kargs &K, uint32_t b, uint64_t frames, uint64_t bytes)
+{
+    pb_count_at(K, b, pb_xcd_region(blockIdx.x, gridDim.x), frames, bytes);
 }
 
 // Folds n workgroup records (pb_count's slot array; pairs = 2: {frames, bytes}, 1: bytes only)
@@ -701,11 +706,18 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
 // frames in both owners measured slower than the linear form (60-B TCP 0.37 vs
 // 0.345 ms, 98-B ICMP 0.70 vs 0.64), so they keep pb_small_kernel.
 
-template <int NDW, int PROTO, bool RANDOM, int WGT = PB_WG> // 64-B frames: WGT / 64 pages per workgroup
-__global__ __launch_bounds__(WGT) void pb_xsmall_kernel(pb_kargs K)
+// pages per workgroup of pb_xsmall_body's LDS tile
+template <int NDW, int WGT>
+constexpr uint32_t pb_xs_npg()
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_tile[(NDW == 16 ? WGT / 64 : PB_XNP_MAX) * PB_XREG / 4];
-    const uint32_t tid = threadIdx.x, b = blockIdx.x;
+    return NDW == 16 ? (uint32_t)WGT / 64u : PB_XNP_MAX;
+}
+
+// workgroup b of nwg (b: the launch's blockIdx.x, or the part's own in pb_batch_kernel)
+template <int NDW, int PROTO, bool RANDOM, int WGT>
+__device__ __forceinline__ void pb_xsmall_body(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
+{
+    const uint32_t tid = threadIdx.x;
     const uint32_t flen = K.fixed_len;
     const uint32_t np = K.xs_np;
     const uint64_t T = K.total_bytes;
@@ -734,12 +746,15 @@ __global__ __launch_bounds__(WGT) void pb_xsmall_kernel(pb_kargs K)
     }
     __syncthreads();
 
-    // page i -> HBM: 256 / WGT 16-B stores per lane per page (one at 256 threads)
-    constexpr uint32_t NPG = NDW == 16 ? (uint32_t)WGT / 64u : PB_XNP_MAX, SPP = 256u / WGT;
+    // page i -> HBM: 256 / WGT 16-B stores per lane per page (one at 256 threads; at 512, lane
+    // t stores chunk t % 256 of every other page)
+    constexpr uint32_t NPG = pb_xs_npg<NDW, WGT>();
+    constexpr uint32_t SPP = WGT >= 256 ? 1u : 256u / WGT, PPS = WGT >= 256 ? (uint32_t)WGT / 256u : 1u;
 #pragma unroll
-    for (uint32_t u = 0; u < NPG * SPP; ++u)
+    for (uint32_t u = 0; u < NPG * SPP / PPS; ++u)
     {
-        const uint32_t i = u / SPP, ch = (u % SPP) * WGT + tid;
+        const uint32_t i = WGT >= 256 ? u * PPS + tid / 256u : u / SPP;
+        const uint32_t ch = WGT >= 256 ? tid % 256u : (u % SPP) * WGT + tid;
         const uint32_t c = c0 + i * cs;
         const uint64_t o = (uint64_t)c * PB_XPG + 16 * ch;
         if (i < np && c < K.xs_nch && o < T)
@@ -765,8 +780,15 @@ __global__ __launch_bounds__(WGT) void pb_xsmall_kernel(pb_kargs K)
             if (c < K.xs_nch)
                 by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
         }
-        pb_count(K, b, 0, by); // fixed length: frames = bytes / length on the host
+        pb_count_at(K, b, pb_xcd_region(b, nwg), 0, by); // fixed length: frames = bytes / length on the host
     }
+}
+
+template <int NDW, int PROTO, bool RANDOM, int WGT = PB_WG> // 64-B frames: WGT / 64 pages per workgroup
+__global__ __launch_bounds__(WGT) void pb_xsmall_kernel(pb_kargs K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[pb_xs_npg<NDW, WGT>() * PB_XREG / 4];
+    pb_xsmall_body<NDW, PROTO, RANDOM, WGT>(K, blockIdx.x, gridDim.x, s_tile);
 }
 
 // XCD-owned pages for frame lengths that are a multiple of 4 but do not divide
@@ -797,11 +819,11 @@ __device__ __forceinline__ uint64_t pb_xp_first_frame64(uint32_t c0, uint32_t fl
     return fa;
 }
 
-template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4 = true> // A4: flen % 4 == 0 (else 2 mod 4)
-__global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
+// s_tile: K.xs_np page regions; workgroup b of nwg as in pb_xsmall_body
+template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4>
+__device__ __forceinline__ void pb_xpage_body(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
 {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[]; // K.xs_np page regions
-    const uint32_t tid = threadIdx.x, b = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
 #if PB_RANGE_LDS
     // (A/B) the CIDR table in LDS: one more barrier before the build
     __shared__ uint2 s_rng[64];
@@ -898,8 +920,59 @@ __global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
             if (c < K.xs_nch)
                 by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
         }
-        pb_count(K, b, 0, by);
+        pb_count_at(K, b, pb_xcd_region(b, nwg), 0, by);
     }
+}
+
+template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4 = true> // A4: flen % 4 == 0 (else 2 mod 4)
+__global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[]; // K.xs_np page regions
+    pb_xpage_body<NDW, PROTO, RANDOM, WGT, A4>(K, blockIdx.x, gridDim.x, s_tile);
+}
+
+// ---------------- several sequences in one launch: pb_batch_kernel ----------------
+//
+// configs[4] builds three sequences per step (64-B UDP, 60-B TCP SYN, 98-B ICMP), each a launch
+// of 2^24 frames of its own page kernel.  Launched back to back or on three streams, every launch
+// pays its own ramp and drain (the mix ran 0.57-0.61 ms per step against 0.55 ms for the three
+// kernels' own times).  Here the three are parts of one grid: part j takes workgroups [o_j, o_j +
+// g_j) (o_j a multiple of 8, so a part's workgroup b stays on XCD b % 8 and keeps its page
+// ownership) and runs its kernel's body on its own kargs; the dispatcher starts part j + 1's
+// workgroups while part j's last ones finish.  One block size (WGT) for all parts: the 64-B part
+// runs pb_xsmall_body with WGT / 64 pages per workgroup.  Kinds (pbk_batch_kind): 1 the 64-B
+// random-payload UDP page kernel, 2 the 60-B random-payload TCP one, 3 the 98-B static-payload ICMP.
+struct pb_batch_args
+{
+    pb_kargs K[3];
+    uint32_t g[3]; // the parts' workgroups
+};
+
+template <int KIND, int WGT>
+__device__ __forceinline__ void pb_batch_part(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
+{
+    if (b >= nwg) // the padding before the next part's first workgroup
+        return;
+    if constexpr (KIND == 1)
+        pb_xsmall_body<16, 17, true, WGT>(K, b, nwg, s_tile);
+    else if constexpr (KIND == 2)
+        pb_xpage_body<16, 6, true, WGT, true>(K, b, nwg, s_tile);
+    else
+        pb_xpage_body<32, 1, false, WGT, false>(K, b, nwg, s_tile);
+}
+
+template <int WGT, int KA, int KB, int KC>
+__global__ __launch_bounds__(WGT) void pb_batch_kernel(pb_batch_args A)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];
+    const uint32_t b = blockIdx.x;
+    const uint32_t o1 = (A.g[0] + 7u) & ~7u, o2 = o1 + ((A.g[1] + 7u) & ~7u);
+    if (b < o1)
+        pb_batch_part<KA, WGT>(A.K[0], b, A.g[0], s_tile);
+    else if (b < o2)
+        pb_batch_part<KB, WGT>(A.K[1], b - o1, A.g[1], s_tile);
+    else
+        pb_batch_part<KC, WGT>(A.K[2], b - o2, A.g[2], s_tile);
 }
 
 // ---------------- group per frame: any length, fixed or packed variable ----------------
@@ -3009,6 +3082,46 @@ static void pbk_launch_small(const pb_kargs *K, uint32_t grid, hipStream_t st)
         pbk_launch_small_p<NDW, 6>(K, grid, st);
     else
         pbk_launch_small_p<NDW, 1>(K, grid, st);
+}
+
+// pb_batch_kernel's part kind of a loaded sequence's kargs (0: no fused form)
+extern "C" int pbk_batch_kind(const pb_kargs *K)
+{
+    if (!K->small_ndw || !K->xs_np || !K->fixed_len || K->pl_cnt != 1)
+        return 0;
+    if (K->small_ndw == 16 && !K->xp && K->proto == 17 && K->pl0.random && K->xs_fp_shift == 6)
+        return 1;
+    if (K->small_ndw == 16 && K->xp && K->proto == 6 && K->pl0.random && K->fixed_len % 4 == 0)
+        return 2;
+    if (K->small_ndw == 32 && K->xp && K->proto == 1 && !K->pl0.random && K->fixed_len % 4 == 2)
+        return 3;
+    return 0;
+}
+
+// One launch of the three parts Ks[0..2], of kinds 1, 2, 3 in that order, each with its page grid
+// (xs_grid) set for block size wgt (256 or 512)
+extern "C" hipError_t pbk_launch_batch(const pb_kargs *Ks, uint32_t wgt, hipStream_t st)
+{
+    pb_batch_args A;
+    size_t lds = 0;
+    uint32_t grid = 0;
+    for (int j = 0; j < 3; ++j)
+    {
+        if (pbk_batch_kind(&Ks[j]) != j + 1 || Ks[j].xs_grid == 0)
+            return hipErrorInvalidValue;
+        A.K[j] = Ks[j];
+        A.g[j] = Ks[j].xs_grid;
+        grid += j < 2 ? (A.g[j] + 7u) & ~7u : A.g[j];
+        const size_t l = (size_t)(j == 0 ? wgt / 64u : Ks[j].xs_np) * PB_XREG + Ks[j].lds_pad;
+        lds = l > lds ? l : lds;
+    }
+    if (wgt == 512)
+        hipLaunchKernelGGL((pb_batch_kernel<512, 1, 2, 3>), dim3(grid), dim3(512), lds, st, A);
+    else if (wgt == 256)
+        hipLaunchKernelGGL((pb_batch_kernel<256, 1, 2, 3>), dim3(grid), dim3(256), lds, st, A);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
 }
 
 // The workgroups pbk_launch_build launches for K (pb_count's records per launch)

@@ -272,6 +272,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pbgpu_frames_alloc": (C.c_int, [P, C.c_uint64, C.c_uint64, C.POINTER(FP)]),
         "pbgpu_frames_free": (None, [P, FP]),
         "pbgpu_build": (C.c_int, [P, C.c_uint16, C.c_uint64, C.c_uint64, FP]),
+        "pbgpu_build_batch": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint16), U64P, U64P, C.POINTER(FP)]),
         "pbgpu_sync": (C.c_int, [P]),
         "pbgpu_frames_total": (C.c_int, [P, FP, U64P]),
         "pbgpu_frames_offsets": (C.c_int, [P, FP]),
@@ -406,6 +407,16 @@ class GpuContext:
 
     def build(self, idx: int, first_iter: int, n_iter: int, fb: FrameBuffer) -> None:
         _check(self.lib.pbgpu_build(self.h, idx, first_iter, n_iter, fb.ptr), "build")
+
+    def build_batch(self, parts) -> None:
+        """parts: (idx, first_iter, n_iter, FrameBuffer) tuples, built as one pbgpu_build_batch
+        call (configs[4]'s three sequences: one fused launch)."""
+        n = len(parts)
+        idx = (C.c_uint16 * n)(*[p[0] for p in parts])
+        fi = (C.c_uint64 * n)(*[p[1] for p in parts])
+        ni = (C.c_uint64 * n)(*[p[2] for p in parts])
+        outs = (C.POINTER(Frames) * n)(*[p[3].ptr for p in parts])
+        _check(self.lib.pbgpu_build_batch(self.h, n, idx, fi, ni, outs), "build_batch")
 
     def sync(self) -> None:
         _check(self.lib.pbgpu_sync(self.h), "sync")

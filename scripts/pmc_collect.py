@@ -23,7 +23,7 @@ for d in sorted(glob.glob(os.path.join(out_dir, "pmc_*"))):
         agg = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"]
-            build = kn.startswith("void pb_") and any(x in kn for x in ("gpf", "stage", "small", "xpage", "vline"))
+            build = kn.startswith("void pb_") and any(x in kn for x in ("gpf", "stage", "small", "xpage", "vline", "batch"))
             aux = kn.startswith("void pb_len_") or kn.startswith("pb_len_") or "pb_scan_blocks" in kn
             fold = "pb_ctr_fold" in kn  # the counters' fold: its bytes spread over the build launches
             aux = aux or fold
@@ -46,6 +46,7 @@ for cfg, e in res["per_launch"].items():
         for a in e["aux"].values():
             hb += a.get("WRITE_SIZE", 0) * 1024 + 2 * a.get("FETCH_SIZE", 0) * 1024
         res["per_launch_hbm_bytes"][cfg] = int(hb)
-        res.setdefault("packets_per_launch", {})[cfg] = 33554432
+        # (c5_mix: 2^24 iterations of each of its three sequences per fused launch)
+        res.setdefault("packets_per_launch", {})[cfg] = 16777216 if cfg == "c5_mix" else 33554432
 json.dump(res, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
 print(json.dumps(res["per_launch_hbm_bytes"], indent=1))

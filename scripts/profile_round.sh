@@ -25,8 +25,9 @@ grep '^{"metric"' $OUT/bench_trace.log > $OUT/bench_under_trace.json
 python3 scripts/trace_summary.py $OUT/bench_trace/run_kernel_trace.csv $OUT/kernel_trace_summary.json
 echo "trace done"
 if [ -z "$SKIP_PMC" ]; then
-  for cfg in c2_udp_64 c2_udp_1500 c3_udp_var c4_tcp_syn c5_icmp_echo; do
-    B="python3 bench.py --steps 5 --warmup 2 --ramp-seconds 0 --no-variants --cpu-seconds 0 --config $cfg --packets 33554432"
+  for cfg in c2_udp_64 c2_udp_1500 c3_udp_var c4_tcp_syn c5_icmp_echo c5_mix; do
+    P=33554432; [ $cfg = c5_mix ] && P=16777216
+    B="python3 bench.py --steps 5 --warmup 2 --ramp-seconds 0 --no-variants --cpu-seconds 0 --config $cfg --packets $P"
     for grp in "WRITE_SIZE" "FETCH_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
       tag=$(echo $grp | cut -d' ' -f1 | tr 'A-Z' 'a-z')
       timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_${cfg}_$tag -o run -- $B > $OUT/pmc_${cfg}_$tag.log 2>&1 || { echo "PMC_FAIL $cfg $grp"; tail -3 $OUT/pmc_${cfg}_$tag.log; exit 1; }

@@ -4,7 +4,8 @@ alternating variants rep by rep to cancel box drift.
 python3 scripts/r04/ab_steps.py CONFIG PACKETS tag:lib[:nbufs[:VAR=a,VAR2=b]] ...
   lib    : libpbgpu.so path relative to the repo ('-' = the in-tree library)
   nbufs  : output buffers per sequence the steps alternate between (default 1)
-Env: REPS (default 6), STEPS (default 40).  CONFIG may be c5_mix (three sequences)."""
+Env: REPS (default 6), STEPS (default 40).  CONFIG may be c5_mix (three sequences); a variant
+with AB_BATCH=1 builds them with one pbgpu_build_batch call per step."""
 import json
 import os
 import sys
@@ -45,14 +46,19 @@ def run(tag, nb, env, k):
     for i, nm in enumerate(names):  # load-time switches (PBGPU_FST_DBG, shapes) take effect
         ctx.load_sequence(i, Sequence.from_config(pc.get(nm)), pc.SEED_BASE)
     bufs = [[ctx.alloc_frames(*ctx.build_size(i, n)) for i in range(len(names))] for _ in range(nb)]
+    def step(first, row):
+        if os.environ.get("AB_BATCH") == "1":
+            ctx.build_batch([(i, first, n, row[i]) for i in range(len(names))])
+        else:
+            for i in range(len(names)):
+                ctx.build(i, first, n, row[i])
+
     for s in range(2 * nb):
-        for i in range(len(names)):
-            ctx.build(i, s * n, n, bufs[s % nb][i])
+        step(s * n, bufs[s % nb])
     ctx.sync()
     ctx.kernel_time()
     for s in range(k):
-        for i in range(len(names)):
-            ctx.build(i, (2 * nb + s) * n, n, bufs[s % nb][i])
+        step((2 * nb + s) * n, bufs[s % nb])
     ctx.sync()
     ms, _ = ctx.kernel_time()
     for row in bufs:
