@@ -89,7 +89,9 @@ def test_bench_mix_under_torchrun_reduces_counters():
     assert gc["bytes"] == [n * steps * 64, n * steps * 60, n * steps * 98]
     assert d["config"]["bytes_per_step_per_gpu"] == n * (64 + 60 + 98)
     assert abs(d["value"] - 3 * n / (d["ms_per_step"] * 1e-3) / 1e6) < 0.01 * d["value"]
-    assert len(d["roofline"]["kernel"]) == 3
+    # one fused launch per step (pbgpu_build_batch), then the three sequences' kernel bodies
+    k = d["roofline"]["kernel"]
+    assert len(k) == 4 and k[0].startswith("pb_batch_kernel<") and all(x.startswith("(part) pb_x") for x in k[1:]), k
 
 
 def test_bench_two_ranks_share_the_gpu_over_gloo():
