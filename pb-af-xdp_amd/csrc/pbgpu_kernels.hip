@@ -170,16 +170,8 @@ __device__ __forceinline__ void pb_st16(uint8_t *p, pb_u32x4 v)
 #define PB_SX_NT 1 // pb_small_kernel's and pb_xpage_kernel's stores are non-temporal
 #endif
 #ifndef PB_FS_NT
-#define PB_FS_NT 0 // (A/B builds) pb_fstage_kernel's stores non-temporal
+#define PB_FS_NT 0 // pb_fstage_kernel's stores non-temporal (its template default; PBGPU_STORE_FLIP=1 the other kind)
 #endif
-__device__ __forceinline__ void pb_st16_fs(uint8_t *p, pb_u32x4 v)
-{
-#if PB_FS_NT
-    __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
-#else
-    pb_st16(p, v);
-#endif
-}
 #ifndef PB_XS_NT
 // pb_xsmall_kernel's stores non-temporal (round 4: 0.333 vs 0.344 ms, 0.334 vs 0.344, 0.342 vs
 // 0.356 per 2^25 64-B frames on three boxes, profiles/r04/ab/ab12-13_*; plain stores had won in
@@ -1608,7 +1600,7 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
 //    pseudo-header word sum minus the generated header bytes of the first payload
 //    chunk (overwritten by the header), so the group reduction is the whole sum.
 //  * Two stage buffers: window w + 1 is generated while window w's stores drain.
-template <int G, bool L4>
+template <int G, bool L4, bool NT = PB_FS_NT != 0> // NT: non-temporal frame stores
 __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
 {
     constexpr uint32_t NGW = PB_WG / G; // frames per window
@@ -1772,13 +1764,13 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
         for (; c + 3 * PB_WG < c1; c += 4 * PB_WG)
         {
             const pb_u32x4 v0 = st16[c], v1 = st16[c + PB_WG], v2 = st16[c + 2 * PB_WG], v3 = st16[c + 3 * PB_WG];
-            pb_st16_fs(gout + 16 * c, v0);
-            pb_st16_fs(gout + 16 * (c + PB_WG), v1);
-            pb_st16_fs(gout + 16 * (c + 2 * PB_WG), v2);
-            pb_st16_fs(gout + 16 * (c + 3 * PB_WG), v3);
+            pb_st16_k<NT>(gout + 16 * c, v0);
+            pb_st16_k<NT>(gout + 16 * (c + PB_WG), v1);
+            pb_st16_k<NT>(gout + 16 * (c + 2 * PB_WG), v2);
+            pb_st16_k<NT>(gout + 16 * (c + 3 * PB_WG), v3);
         }
         for (; c < c1; c += PB_WG)
-            pb_st16_fs(gout + 16 * c, st16[c]);
+            pb_st16_k<NT>(gout + 16 * c, st16[c]);
         if (tid == PB_WG - 1 && (R1 & 15u))
         {
             const uint32_t *sw = reinterpret_cast<const uint32_t *>(stg) + 4 * c1;
@@ -3177,13 +3169,16 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
         const uint32_t grid = (uint32_t)((K->n_frames + K->fst_wgf - 1) / K->fst_wgf);
         const size_t lds = (size_t)K->fst_nbuf * K->fst_sb + PB_FST_LDS(K->fst_wgf) + K->lds_pad;
         const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
-#define PB_FST(GG)                                                                                    \
-    do                                                                                                \
-    {                                                                                                 \
-        if (l4)                                                                                       \
-            hipLaunchKernelGGL((pb_fstage_kernel<GG, true>), dim3(grid), dim3(PB_WG), lds, st, *K);  \
-        else                                                                                          \
-            hipLaunchKernelGGL((pb_fstage_kernel<GG, false>), dim3(grid), dim3(PB_WG), lds, st, *K); \
+#define PB_FST(GG)                                                                                        \
+    do                                                                                                    \
+    {                                                                                                     \
+        constexpr bool NT = PB_FS_NT != 0;                                                                \
+        if (l4 && K->store_flip) /* (experiments) the other store kind */                                \
+            hipLaunchKernelGGL((pb_fstage_kernel<GG, true, !NT>), dim3(grid), dim3(PB_WG), lds, st, *K); \
+        else if (l4)                                                                                      \
+            hipLaunchKernelGGL((pb_fstage_kernel<GG, true>), dim3(grid), dim3(PB_WG), lds, st, *K);      \
+        else                                                                                              \
+            hipLaunchKernelGGL((pb_fstage_kernel<GG, false>), dim3(grid), dim3(PB_WG), lds, st, *K);     \
     } while (0)
         if (K->fst_g == 16)
             PB_FST(16);
