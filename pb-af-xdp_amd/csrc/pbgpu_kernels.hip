@@ -174,8 +174,8 @@ __device__ __forceinline__ void pb_st16(uint8_t *p, pb_u32x4 v)
 #endif
 #ifndef PB_XS_NT
 // pb_xsmall_kernel's stores non-temporal (round 4: 0.333 vs 0.344 ms, 0.334 vs 0.344, 0.342 vs
-// 0.356 per 2^25 64-B frames on three boxes, profiles/r04/ab/ab12-13_*; plain stores had won in
-// round 3, when each workgroup still added its counts with memory-side atomics)
+// 0.356 and 0.3325 vs 0.3287 per 2^25 64-B frames on four boxes, profiles/r04/ab/ab12-13_*;
+// plain stores had won in round 3, when each workgroup still added its counts with atomics)
 #define PB_XS_NT 1
 #endif
 __device__ __forceinline__ void pb_st16_xs(uint8_t *p, pb_u32x4 v)
