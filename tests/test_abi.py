@@ -62,3 +62,4 @@ def test_null_arguments_rejected():
     assert lib.pbgpu_open(0, None) == -22
     assert lib.pbgpu_build(None, 0, 0, 1, None) == -22
     assert lib.pbgpu_load_sequence(None, 0, None, None, None, None, 0) == -22
+    assert lib.pbgpu_build_batch(None, 0, None, None, None, None) == -22
