@@ -142,6 +142,9 @@ struct frames_events
     unsigned long long *d_rstart = nullptr;
     bool packed32 = false;
     uint32_t wf = 0;
+    // pb_xsmall_kernel's occupancy measured on this buffer (tune_xsmall): -1 not yet, 0 uncapped,
+    // else the dynamic LDS that caps it
+    int xs_pad = -1;
 };
 
 frames_events *frames_ev(pbgpu_frames *f)
@@ -173,6 +176,9 @@ struct pbgpu_ctx
     int timing_mode = PBGPU_TIMING_LAUNCH;
     timing_pair span = {nullptr, nullptr}; // PBGPU_TIMING_SPAN: first-launch / call events
     uint32_t span_n = 0;                    // launches in the open span (0: none open)
+    uint32_t *d_tune_slots = nullptr; // tune_xsmall's count records (never folded)
+    int xs_tuned_last = -1;           // the last 64-B build's tuned cap (pbgpu_kernel_name)
+    uint32_t tune_cap = 0;
     // PBGPU_TIMING_SPAN: the builds of sequence i run on seq_stream[i % PB_SEQ_STREAMS], so the
     // kernels of different sequences overlap (as the reference's non-blocking sequences run
     // their threads side by side, sequence.c:741-765); every other call first joins them
@@ -606,6 +612,8 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipFree(ctx->d_jump);
     if (ctx->d_lcg48)
         (void)hipFree(ctx->d_lcg48);
+    if (ctx->d_tune_slots)
+        (void)hipFree(ctx->d_tune_slots);
     if (ctx->d_orbit)
         (void)hipFree(ctx->d_orbit);
     if (ctx->d_dbg)
@@ -1346,6 +1354,62 @@ static void report_phase_timing(pbgpu_ctx *ctx, uint64_t n_wg)
             life / (double)(t1 - t0));
 }
 
+// pb_xsmall_kernel's occupancy, chosen per frame buffer.  With non-temporal stores the 64-B page
+// kernel capped at 5 workgroups per CU runs 0.309-0.311 ms per 2^25 frames in some buffers and
+// 0.35-0.36 in others, where the uncapped shape runs 0.33 in all (profiles/r04/ab/ab17_*, ab18_*:
+// the cap's rate depends on the buffer's placement, as the region kernels' do).
+// So the first build of >= 2^22 64-B frames into a buffer times both shapes on it (after a
+// warm-up, 3 alternating rounds of 20 launches: the same frames; count records into a scratch
+// array) and keeps the cap for that buffer if it is >= 1% faster.  Synchronous, once per buffer
+// (~0.07 s at 2^25 frames); PBGPU_XS_TUNE=0 skips it (uncapped), PBGPU_LDS_PAD overrides it.
+#define PB_XS_TUNE_PAD (32768u - 4u * PB_XREG) // 17-KiB tile + pad = 32 KiB: 5 workgroups per CU
+static int tune_xsmall(pbgpu_ctx *ctx, const pb_kargs &K, hipStream_t st, int *xs_pad)
+{
+    pb_kargs T = K;
+    if (ctx->d_tune_slots == nullptr || ctx->tune_cap < T.xs_grid)
+    {
+        if (ctx->d_tune_slots)
+            (void)hipFree(ctx->d_tune_slots);
+        ctx->d_tune_slots = nullptr;
+        ctx->tune_cap = 0;
+        HIPCHK(hipMalloc((void **)&ctx->d_tune_slots, (size_t)T.xs_grid * sizeof(uint32_t)));
+        ctx->tune_cap = T.xs_grid;
+    }
+    T.ctr_slots = ctx->d_tune_slots;
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    const uint32_t pads[2] = {0u, PB_XS_TUNE_PAD};
+    double best[2] = {1e30, 1e30};
+    hipError_t e = hipSuccess;
+    // 80 untimed launches bring the clocks up (the first ~60 ms of a run are slower), then three
+    // rounds of 20 back-to-back launches per shape (the cap's effect shows under sustained load)
+    for (int i = 0; i < 80 && e == hipSuccess; ++i)
+        e = pbk_launch_build(&T, st);
+    for (int r = 0; r < 3 && e == hipSuccess; ++r)
+        for (int v = 0; v < 2 && e == hipSuccess; ++v)
+        {
+            T.lds_pad = pads[v];
+            e = hipEventRecord(a, st);
+            for (int i = 0; i < 20 && e == hipSuccess; ++i)
+                e = pbk_launch_build(&T, st);
+            if (e == hipSuccess)
+                e = hipEventRecord(b, st);
+            if (e == hipSuccess)
+                e = hipEventSynchronize(b);
+            float ms = 0.f;
+            if (e == hipSuccess)
+                e = hipEventElapsedTime(&ms, a, b);
+            if (e == hipSuccess)
+                best[v] = ms / 20 < best[v] ? ms / 20 : best[v];
+        }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    HIPCHK(e);
+    *xs_pad = best[1] < 0.99 * best[0] ? (int)pads[1] : 0;
+    return PBGPU_OK;
+}
+
 // The frames' build-completion event (kept in pbgpu_frames.reserved): the
 // landing stream waits on it, so landing one buffer overlaps building the next.
 static int mark_built(pbgpu_ctx *ctx, pbgpu_frames *out, hipStream_t st)
@@ -1567,6 +1631,16 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
         bp->K = K;
         bp->built = true;
         return PBGPU_OK;
+    }
+    // pb_xsmall_kernel: the occupancy measured on this buffer (tune_xsmall)
+    if (K.small_ndw == 16 && K.xs_grid && !K.xp && K.lds_pad == 0 && getenv("PBGPU_LDS_PAD") == NULL &&
+        !env_is("PBGPU_XS_TUNE", "0"))
+    {
+        if (fe->xs_pad < 0 && nf >= (1u << 22) && (rc = tune_xsmall(ctx, K, st, &fe->xs_pad)) != PBGPU_OK)
+            return rc;
+        if (fe->xs_pad > 0)
+            K.lds_pad = (uint32_t)fe->xs_pad;
+        ctx->xs_tuned_last = fe->xs_pad;
     }
     timing_pair tp = {nullptr, nullptr};
     if (!span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
@@ -2285,8 +2359,8 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_xpage_kernel<%u, %u, %s, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
                  K.xp_wgt, K.fixed_len % 4 == 0 ? "true" : "false");
     else if (K.xs_np && !env_is("PBGPU_KERNEL", "linear"))
-        snprintf(buf, n, "pb_xsmall_kernel<%u, %u, %s, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
-                 (uint32_t)PB_WG);
+        snprintf(buf, n, "pb_xsmall_kernel<%u, %u, %s, %u>%s", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
+                 (uint32_t)PB_WG, ctx->xs_tuned_last > 0 && K.small_ndw == 16 ? " (5 wg/CU, tuned)" : "");
     else
         snprintf(buf, n, "pb_small_kernel<%u, %u, %s, %u, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
                  K.small_wgt ? K.small_wgt : (uint32_t)PB_WG, K.fixed_len % 4 == 2 ? 2u : 0u);

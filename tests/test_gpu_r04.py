@@ -64,3 +64,26 @@ def test_counter_ring_matches_the_atomic_form(monkeypatch):
     atomic = _run(monkeypatch, atomic=True, launches=6)
     for r, a in zip(ring, atomic):
         assert np.array_equal(r, a)
+
+
+def test_xsmall_occupancy_tuning_keeps_frames_and_counts(monkeypatch):
+    """The first >= 2^22-frame 64-B build times the uncapped and the 5-per-CU shape (tune_xsmall)
+    into the caller's buffer: the frames equal an untuned build's and the calibration launches
+    are not counted."""
+    n = 1 << 22
+    seq = Sequence.from_config(pc.get("c2_udp_64"))
+    out = []
+    for tune in ("1", "0"):
+        monkeypatch.setenv("PBGPU_XS_TUNE", tune)
+        with GpuContext(0) as ctx:
+            ctx.load_sequence(0, seq, pc.SEED_BASE)
+            fb = ctx.alloc_frames(*ctx.build_size(0, n))
+            ctx.build(0, 777, n, fb)
+            ctx.build(0, 777, n, fb)
+            ctx.sync()
+            p, b = ctx.counters(1)
+            assert int(p[0]) == 2 * n and int(b[0]) == 2 * n * 64
+            out.append((ctx.kernel_name(0), fb.packed()))
+            fb.free()
+    assert out[0][0].startswith("pb_xsmall_kernel<16, 17, true, 256>") and not out[1][0].endswith("tuned)")
+    assert np.array_equal(out[0][1], out[1][1])
