@@ -85,8 +85,9 @@ def init_dist(n_gpus):
         # round-robin, counters and timings reduce over gloo); the bench itself is RCCL
         backend = os.environ.get("PB_DIST_BACKEND", "nccl")
         if backend == "gloo":
-            local %= max(1, torch.cuda.device_count())
-            torch.cuda.set_device(local)
+            if torch.cuda.is_available():
+                local %= max(1, torch.cuda.device_count())
+                torch.cuda.set_device(local)
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
@@ -94,12 +95,18 @@ def init_dist(n_gpus):
     return dist, world, rank, local
 
 
+def reduce_device(local):
+    """Where the collectives' tensors live: the rank's GPU under RCCL, host memory under gloo."""
+    return "cpu" if os.environ.get("PB_DIST_BACKEND", "nccl") == "gloo" else f"cuda:{local}"
+
+
 def barrier(dist, local):
     if dist is not None:
         import torch
 
         dist.barrier()
-        torch.cuda.synchronize(local)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(local)
 
 
 def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ramp_s=0.0, launch_reps=0):
@@ -162,7 +169,7 @@ def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ram
     counters = None
     if dist is not None:
         # RCCL over xGMI: the global sent-packet / byte counters of the timed steps
-        gp, gb = pb_dist.allreduce_counters(dp, db, device=f"cuda:{local}")
+        gp, gb = pb_dist.allreduce_counters(dp, db, device=reduce_device(local))
         counters = {"packets": gp, "bytes": gb}
         if gp != [steps * n_pkts * world] * nseq:
             raise SystemExit(f"global counter mismatch: {gp} frames for {world} x {steps} x {n_pkts} per sequence")
@@ -196,7 +203,7 @@ def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ram
     if dist is not None:
         import torch
 
-        w = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
+        w = torch.tensor([wall], dtype=torch.float64, device=reduce_device(local))
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
     return {"wall_s": wall, "span_ms_per_step": k_ms / max(steps, 1), "kernel_launches": k_n, "flens": flens,

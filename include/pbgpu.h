@@ -114,8 +114,9 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
  * its sequences side by side (sequence.c:741-762, one thread group per
  * sequence); configs[4]'s three (64-B UDP, 60-B TCP SYN, 98-B ICMP echo, each
  * into its own 4-KiB-aligned buffer) are built by one fused launch
- * (pb_batch_kernel), any other set by one launch per part.  PBGPU_BATCH=0:
- * always one launch per part. */
+ * (pb_batch_kernel), any other set by one launch per part (also when a part's
+ * sequence was loaded with PBGPU_BATCH=0).  Every part's arguments are checked
+ * first: on an error no part is built and the counters are unchanged. */
 int pbgpu_build_batch(pbgpu_ctx *ctx, uint32_t n, const uint16_t *seq_idx, const uint64_t *first_iter,
                       const uint64_t *n_iter, pbgpu_frames *const *outs);
 

@@ -104,7 +104,6 @@ struct pb_kargs
     uint32_t stage_bytes;   // its LDS stage size (multiple of 16, >= W + longest frame + 32)
     uint32_t stage_wgf;     // its frames per workgroup (<= its threads per workgroup)
     uint32_t stage_wgt;     // its threads per workgroup: 256, or 64 (one wave, barriers are wave-local)
-    unsigned long long *dbg; // PB_TIMING builds only: per-workgroup phase timestamps
     const uint2 *lcg48;     // lcg48[m] = L^(48 m): one 16-B chunk of payload = 48 LCG steps
     uint32_t stail[32];     // small kernel, static payload: payload bytes at frame dwords p0.. (p0 = (hl-2)/4)
     // XCD-owned small kernel (pb_xsmall_kernel), frame lengths dividing 4096: pages of 4 KiB hold
@@ -127,16 +126,10 @@ struct pb_kargs
     uint32_t fst_sb;        // bytes per stage buffer (multiple of 16)
     uint32_t fst_nbuf;      // stage buffers: 2 (window w + 1 is built while w streams out) or 1
     uint32_t vst;           // 1: the stage_* shape runs pb_vstage_kernel (every payload random, stream rule)
-    uint32_t fst_dbg;       // diagnostics (PBGPU_FST_DBG, wrong output): bit 0 skips payload + headers,
-                            // bit 1 the stores, bit 3 phase A (time decomposition);
-                            // pb_vline_kernel: bit 0 the stream, bit 2 its arithmetic (constant stores),
-                            // bit 4 the prologue (constant stores over the launch's regions), bit 5
-                            // the payload sums (no orbit-table reads), bit 6 the orbit-table reads
-                            // alone (sums computed from the entries' indices);
-                            // pb_vstage_kernel: bit 4 fixed 8-lane groups, bit 5 no 32-lane groups, bit 6 workgroup
-                            // edges at frame starts, bit 8 no longest-first window order (A/B)
-    uint32_t lds_pad;       // dynamic LDS added to the build launch: caps workgroups per CU (fewer
-                            // concurrent writers)
+    uint32_t vst_shape;     // pb_vstage_kernel shape options (PBGPU_VST_SHAPE; each parity-tested): bit 4 fixed
+                            // 8-lane groups, bit 5 no 32-lane groups, bit 6 workgroup edges at frame starts,
+                            // bit 8 no longest-first window order
+    uint32_t lds_pad;       // dynamic LDS added to the build launch: caps its workgroups per CU
     // pb_vstage_kernel, variable length: per-workgroup length sums (stage_wgf frames each) and
     // their exclusive scan per 256 workgroups (pb_len_wgsum + pb_scan_blocks); the kernel then
     // writes offsets_w for its own frames.  Null: offsets[] was scanned beforehand (3 passes).
@@ -161,14 +154,10 @@ struct pb_kargs
     // pb_xpage_kernel: 1 when the launch's last page index times 4096 % flen reaches 2^31 (the
     // first frame of a page then takes the 64-bit path)
     uint32_t xp_fa_hi;
-    // (experiments) pb_xcd_region's rotation for the region-walking kernels: XCD x starts its
-    // contiguous eighth x * xcd_rot / 256 of an eighth in (0: at its first region)
-    uint32_t xcd_rot;
     // this launch's per-workgroup counts (pb_count): u32 bytes per workgroup for fixed-length
     // sequences, {frames, bytes} for variable ones, at position pb_xcd_region(blockIdx.x); the
     // host folds them into `counters` (pb_ctr_fold).  Null: one atomic per workgroup instead.
     uint32_t *ctr_slots;
-    uint32_t store_flip;    // (experiments, PBGPU_STORE_FLIP=1) pb_vline_kernel / pb_small_kernel: the other store kind
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)
@@ -179,31 +168,13 @@ struct pb_kargs
 #define PB_VST_PRO 576 // pb_vstage_kernel prologue records: 16 jump entries, 12 starts / S0 parts, 4 wave sums, template, 17 chunk masks (16-B multiple)
 #define PB_VST_HV0 4u  // per-frame header dwords kept in LDS: [4, 13) = IPv4 from tot_len to the L4 checksum
 #define PB_VST_HVN 9u  // (UDP csum dword 10, TCP 12, ICMP 9); dwords 0-3 and 13-15 are the template's
-// each XCD builds one contiguous eighth of a launch's workgroup regions (pb_xcd_region)
-#ifndef PB_FST_XREMAP
-#define PB_FST_XREMAP 1
-#endif
-#ifndef PB_VST_XREMAP
-#define PB_VST_XREMAP 1
-#endif
-#ifndef PB_SMALL_XREMAP
-#define PB_SMALL_XREMAP 1 // pb_small_kernel: XCD-contiguous regions (98-B ICMP 0.60 -> 0.47 ms, profiles/r03/ab)
-#endif
-#ifndef PB_XS_XREMAP
-#define PB_XS_XREMAP 0
-#endif
 #define PB_VST_CAP(wgf) (((size_t)(wgf) + PB_VST_GHOSTS + 1) & ~(size_t)1)
 // pb_vline_kernel's LDS: 256 B of prologue records, then per frame slot (own + ghosts) a 16-B
 // record and nsp 16-B header chunks, a zero chunk and 17 chunk masks, the lcg48 entries, the
 // line map (u16)
 #define PB_VL_STEP 16384u // bytes of a workgroup's region per step (4 waves x 4 KiB)
-#ifndef PB_ORB_SH
 #define PB_ORB_SH 5 // orbit prefix sums sampled every 2^PB_ORB_SH positions (2 MiB table)
-#endif
-#ifndef PB_VL_MT
-#define PB_VL_MT 1 // pb_vline_kernel's chunk masks: one table row per (plo + phi) (0: two rows, ANDed)
-#endif
-#define PB_VL_NMASK (PB_VL_MT ? 33 : 17)
+#define PB_VL_NMASK 33 // pb_vline_kernel's chunk masks: one table row per (plo + phi)
 #define PB_VL_LDS(wgf, nsp, nl48, nlines)                                                                       \
     ((size_t)256 + ((size_t)(wgf) + PB_VST_GHOSTS) * 16 * (1 + (size_t)(nsp)) + (1 + PB_VL_NMASK) * 16 +         \
      (size_t)(nl48) * 8 +                                                                                        \

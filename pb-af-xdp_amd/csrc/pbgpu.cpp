@@ -68,16 +68,98 @@ static uint64_t scan_tmp_bytes(uint64_t capacity_frames)
 namespace
 {
 
-bool env_is(const char *name, const char *value)
+// Shape overrides for the parity tests and A/B runs (PBGPU_* environment).  They are read in
+// one place, read_opts(): at pbgpu_open into the context (landing and batch options) and at
+// pbgpu_load_sequence into the slot (kernel shapes), so the build path never reads the
+// environment and a loaded sequence's shape is fixed.  Every selectable shape is parity-tested
+// (tests/test_gpu_kernels.py).
+enum pb_kern_force
+{
+    PBO_K_AUTO = 0,
+    PBO_K_GPF,    // PBGPU_KERNEL=gpf: the group-per-frame kernel for frames > 128 B
+    PBO_K_STAGE,  // =stage: pb_stage_kernel
+    PBO_K_VSTAGE, // =vstage: pb_vstage_kernel for packed variable lengths
+    PBO_K_NOPAGE, // =nopage: no pb_xpage_kernel (linear small kernel)
+    PBO_K_LINEAR, // =linear: neither page kernel
+};
+
+struct pb_opts
+{
+    int kernel = PBO_K_AUTO;
+    uint32_t g = 0;          // PBGPU_G: lanes per frame of the staged / group kernels (8, 16, 32, 64)
+    uint32_t fpw = 0;        // PBGPU_FPW: frames per workgroup of the group kernel / staged window
+    uint32_t wgt = 0;        // PBGPU_WGT=64: one-wave staged workgroups
+    uint32_t wgf = 0;        // PBGPU_WGF: staged frames per workgroup
+    uint32_t stage_kb = 0;   // PBGPU_STAGE_KB: staged window
+    uint32_t small_wgt = 0;  // PBGPU_SMALL_WGT: linear small kernel's workgroup (64 / 128 / 256)
+    uint32_t fst_g = 0, fst_wgf = 0, fst_nbuf = 0; // PBGPU_FST_G / _WGF / _NBUF
+    uint32_t vl_wgf = 0;     // PBGPU_VL_WGF: pb_vline_kernel's own frames per workgroup
+    uint32_t vst_shape = 0;  // PBGPU_VST_SHAPE: pb_vstage_kernel shape bits (pb_kargs.vst_shape)
+    bool vst_scan3 = false;  // PBGPU_VST_SCAN=3pass: pb_vstage_kernel after the 3-pass length scan
+    bool xp_force = false;   // PBGPU_XP_FORCE=1: pb_xpage_kernel for every even length <= 128 B
+    bool xp_static = true;   // PBGPU_XP_STATIC=0: no page kernel for static payloads
+    bool xp_fa64 = false;    // PBGPU_XP_FA64=1: pb_xpage_kernel's 64-bit first-frame path at any size
+    uint32_t xp_wgt = 0;     // PBGPU_XP_WGT: 256 / 512
+    uint32_t xp_np = 0;      // PBGPU_XP_NP: pages per workgroup
+    bool ctr_atomic = false; // PBGPU_CTR_ATOMIC=1: counts by one atomic per workgroup, no record ring
+    uint32_t ctr_ring = 0;   // PBGPU_CTR_RING: record ring words (small: the fold-when-full path)
+    bool batch = true;       // PBGPU_BATCH=0: pbgpu_build_batch launches every part on its own
+    uint32_t batch_wgt = 512; // PBGPU_BATCH_WGT=256: pb_batch_kernel's 256-thread form
+    bool seq_streams = true; // PBGPU_SEQ_STREAMS=0: span-mode builds all on the context's stream
+    bool land_spin = true;   // PBGPU_LAND_SPIN=0: blocking landing waits
+    bool umem_dma = false;   // PBGPU_UMEM_DMA=1: land through DMA copies, not the mapped scatter
+};
+
+uint32_t opt_u32(const char *name)
+{
+    const char *e = getenv(name);
+    return e != NULL && atoi(e) > 0 ? (uint32_t)atoi(e) : 0u;
+}
+
+bool opt_is(const char *name, const char *value)
 {
     const char *e = getenv(name);
     return e != NULL && strcmp(e, value) == 0;
 }
 
-int env_int(const char *name, int dflt)
+pb_opts read_opts()
 {
-    const char *e = getenv(name);
-    return e != NULL && atoi(e) > 0 ? atoi(e) : dflt;
+    pb_opts o;
+    const char *k = getenv("PBGPU_KERNEL");
+    if (k)
+        o.kernel = !strcmp(k, "gpf") ? PBO_K_GPF
+                   : !strcmp(k, "stage") ? PBO_K_STAGE
+                   : !strcmp(k, "vstage") ? PBO_K_VSTAGE
+                   : !strcmp(k, "nopage") ? PBO_K_NOPAGE
+                   : !strcmp(k, "linear") ? PBO_K_LINEAR
+                                          : PBO_K_AUTO;
+    o.g = opt_u32("PBGPU_G");
+    if (o.g != 8 && o.g != 16 && o.g != 32 && o.g != 64)
+        o.g = 0;
+    o.fpw = opt_u32("PBGPU_FPW");
+    o.wgt = opt_u32("PBGPU_WGT");
+    o.wgf = opt_u32("PBGPU_WGF");
+    o.stage_kb = opt_u32("PBGPU_STAGE_KB");
+    o.small_wgt = opt_u32("PBGPU_SMALL_WGT");
+    o.fst_g = opt_u32("PBGPU_FST_G");
+    o.fst_wgf = opt_u32("PBGPU_FST_WGF");
+    o.fst_nbuf = opt_u32("PBGPU_FST_NBUF");
+    o.vl_wgf = opt_u32("PBGPU_VL_WGF");
+    o.vst_shape = opt_u32("PBGPU_VST_SHAPE");
+    o.vst_scan3 = opt_is("PBGPU_VST_SCAN", "3pass");
+    o.xp_force = opt_is("PBGPU_XP_FORCE", "1");
+    o.xp_static = !opt_is("PBGPU_XP_STATIC", "0");
+    o.xp_fa64 = opt_is("PBGPU_XP_FA64", "1");
+    o.xp_wgt = opt_u32("PBGPU_XP_WGT");
+    o.xp_np = opt_u32("PBGPU_XP_NP");
+    o.ctr_atomic = opt_is("PBGPU_CTR_ATOMIC", "1");
+    o.ctr_ring = opt_u32("PBGPU_CTR_RING");
+    o.batch = !opt_is("PBGPU_BATCH", "0");
+    o.batch_wgt = opt_u32("PBGPU_BATCH_WGT") == 256 ? 256u : 512u;
+    o.seq_streams = !opt_is("PBGPU_SEQ_STREAMS", "0");
+    o.land_spin = !opt_is("PBGPU_LAND_SPIN", "0");
+    o.umem_dma = getenv("PBGPU_UMEM_DMA") != NULL;
+    return o;
 }
 
 int verbose()
@@ -117,6 +199,7 @@ struct seq_slot
     uint64_t ctr_cap = 0, ctr_used = 0, ctr_pairs = 1; // words; words per record
     hipStream_t ctr_last = nullptr; // the stream of the last launch that wrote or folded the ring
     hipEvent_t ctr_ev = nullptr;
+    pb_opts opt; // shape overrides, read when the sequence was loaded
 };
 
 struct timing_pair
@@ -142,9 +225,6 @@ struct frames_events
     unsigned long long *d_rstart = nullptr;
     bool packed32 = false;
     uint32_t wf = 0;
-    // pb_xsmall_kernel's occupancy measured on this buffer (tune_xsmall): -1 not yet, 0 uncapped,
-    // else the dynamic LDS that caps it
-    int xs_pad = -1;
 };
 
 frames_events *frames_ev(pbgpu_frames *f)
@@ -162,13 +242,11 @@ struct pbgpu_ctx
     hipStream_t stream = nullptr;      // frame builds
     hipStream_t land_stream = nullptr; // UMEM landing: overlaps the next build (pbgpu_copy_to_umem)
     bool land_events = false;          // set by the first landing: builds then record a completion event
-    bool land_spin = true;             // pbgpu_land_wait polls (PBGPU_LAND_SPIN=0: blocking waits)
+    pb_opts opt;                       // read at pbgpu_open: landing, stream and batch options
     uint2 *d_jump = nullptr;
     uint2 *d_lcg48 = nullptr;
     uint32_t *d_orbit = nullptr; // pb_vline_kernel: LCG-orbit prefix sums (built on first use, 2 MiB)
     uint32_t orbit_tot = 0;
-    unsigned long long *d_dbg = nullptr; // PBGPU_TIMING: per-workgroup phase stamps
-    uint64_t dbg_cap = 0;
     unsigned long long *d_counters = nullptr; // [PB_MAX_SEQUENCES][PB_CTR_SHARDS][PB_CTR_STRIDE]
     seq_slot seqs[PB_MAX_SEQUENCES];
     std::vector<timing_pair> pending;
@@ -176,9 +254,6 @@ struct pbgpu_ctx
     int timing_mode = PBGPU_TIMING_LAUNCH;
     timing_pair span = {nullptr, nullptr}; // PBGPU_TIMING_SPAN: first-launch / call events
     uint32_t span_n = 0;                    // launches in the open span (0: none open)
-    uint32_t *d_tune_slots = nullptr; // tune_xsmall's count records (never folded)
-    int xs_tuned_last = -1;           // the last 64-B build's tuned cap (pbgpu_kernel_name)
-    uint32_t tune_cap = 0;
     // PBGPU_TIMING_SPAN: the builds of sequence i run on seq_stream[i % PB_SEQ_STREAMS], so the
     // kernels of different sequences overlap (as the reference's non-blocking sequences run
     // their threads side by side, sequence.c:741-765); every other call first joins them
@@ -419,6 +494,18 @@ int upload(T **dptr, const T *src, size_t n)
     return PBGPU_OK;
 }
 
+// Dynamic LDS that caps a launch at per_cu workgroups per CU: total LDS per workgroup just over
+// 160 KiB / (per_cu + 1).  (The measured shape: 64-B pages with 41,384 B per workgroup ran 0.29-0.30
+// ms per 2^25 frames, with 46,592 B 0.35 ms like 2 per CU, profiles/r05/ab/xs9.jsonl, so the
+// point just past the next count's boundary is the one to take.)
+#define PB_LDS_PER_CU (160u * 1024u)
+#define PB_XS_WG_PER_CU 3 // pb_xsmall_kernel
+uint32_t lds_cap_pad(uint32_t static_bytes, uint32_t per_cu)
+{
+    const uint32_t target = PB_LDS_PER_CU / (per_cu + 1u) + 512u;
+    return target > static_bytes ? target - static_bytes : 0u;
+}
+
 void slot_free(seq_slot &s)
 {
     if (s.d_ranges)
@@ -541,7 +628,7 @@ int pbgpu_open(int device, pbgpu_ctx **out)
     HIPCHK(hipSetDevice(device));
     pbgpu_ctx *ctx = new pbgpu_ctx();
     ctx->device = device;
-    ctx->land_spin = !env_is("PBGPU_LAND_SPIN", "0");
+    ctx->opt = read_opts();
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->land_stream, hipStreamNonBlocking) != hipSuccess)
     {
@@ -612,12 +699,8 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipFree(ctx->d_jump);
     if (ctx->d_lcg48)
         (void)hipFree(ctx->d_lcg48);
-    if (ctx->d_tune_slots)
-        (void)hipFree(ctx->d_tune_slots);
     if (ctx->d_orbit)
         (void)hipFree(ctx->d_orbit);
-    if (ctx->d_dbg)
-        (void)hipFree(ctx->d_dbg);
     if (ctx->d_counters)
         (void)hipFree(ctx->d_counters);
     if (ctx->h_stage)
@@ -678,6 +761,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         S.ctr_last = ctx->stream;
     }
 
+    const pb_opts O = read_opts();
     pb_rules_t R = {PB_PAYLOAD_STREAM, PB_FOLD_FULL};
     if (rules)
         R = *rules;
@@ -943,19 +1027,22 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             // regions end on 128-B lines), measured 2.5% faster than 256 on the 98-B ICMP frame
             // (0.649 vs 0.666 ms per 2^25 frames; 128: 0.666; profiles/r02/ab/small_wgt_icmp98.txt);
             // odd lengths keep 256 (line-aligned regions).  PBGPU_SMALL_WGT = 64 / 128 / 256 overrides
-            const int w = env_int("PBGPU_SMALL_WGT", minf % 2 == 0 ? 64 : 256);
-            K.small_wgt = (w == 64 || w == 128) ? (uint32_t)w : 0u;
+            const uint32_t w = O.small_wgt ? O.small_wgt : (minf % 2 == 0 ? 64u : 256u);
+            K.small_wgt = (w == 64 || w == 128) ? w : 0u;
         }
-        const bool xp_force = env_is("PBGPU_XP_FORCE", "1"); // experiments: pb_xpage_kernel for any length % 4 == 0
+        const bool xp_force = O.xp_force; // pb_xpage_kernel for any even length
         if (4096 % minf == 0 && minf == 4 * K.small_ndw && !xp_force) // pages of whole frames: pb_xsmall_kernel (64 / 128 B)
         {
             while ((minf << K.xs_fp_shift) < 4096)
                 ++K.xs_fp_shift;
             K.xs_np = 256 >> K.xs_fp_shift;
+            // one wave per page is fastest with few waves per CU (profiles/r05/ab/xs9.jsonl):
+            // 64-B frames 0.297-0.303 ms per 2^25 at 3 workgroups per CU, 0.323-0.329 uncapped
+            K.lds_pad = lds_cap_pad(K.xs_np * PB_XPG, PB_XS_WG_PER_CU);
         }
         else if ((xp_force && minf % 2 == 0) ||
-                 (!env_is("PBGPU_KERNEL", "nopage") && minf % 2 == 0 && minf >= 52 && minf <= 128 &&
-                  (minf % 4 == 0 && minf <= 64 ? true : !pls[0].random && !env_is("PBGPU_XP_STATIC", "0"))))
+                 (O.kernel != PBO_K_NOPAGE && minf % 2 == 0 && minf >= 52 && minf <= 128 &&
+                  (minf % 4 == 0 && minf <= 64 ? true : !pls[0].random && O.xp_static)))
         {
             // XCD-owned 4 KiB pages for frames cut at the page edges (pb_xpage_kernel): one slot
             // per frame touching a page, 512-thread workgroups (one pass of slots): lengths of
@@ -972,12 +1059,11 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             K.xp_fpp = (4096 + minf - 1) / minf + 1;
             K.xp_div = make_div(K.xp_fpp);
             K.xp_inv = 1.0 / (double)minf;
-            K.xp_wgt = (uint32_t)env_int("PBGPU_XP_WGT", 512) == 256 ? 256 : 512;
+            K.xp_wgt = O.xp_wgt == 256 ? 256 : 512;
             const uint32_t want = minf % 4 == 2 ? 9u : 7u;
             K.xs_np = std::max<uint32_t>(1, std::min<uint32_t>(want, 2 * PB_WG / K.xp_fpp));
-            const int enp = env_int("PBGPU_XP_NP", 0); // at most two frame slots per 256 lanes
-            if (enp > 0 && (uint32_t)enp * K.xp_fpp <= 2 * PB_WG)
-                K.xs_np = (uint32_t)enp;
+            if (O.xp_np && O.xp_np * K.xp_fpp <= 2 * PB_WG) // at most two frame slots per 256 lanes
+                K.xs_np = O.xp_np;
         }
         if (!pls[0].random)
         {
@@ -990,7 +1076,6 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
         }
     }
     {
-        const char *kern = getenv("PBGPU_KERNEL");
         if (!K.small_ndw)
         {
             // lanes per frame (measured, profiles/r01/gsweep): equal-length frames take
@@ -1013,15 +1098,11 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             {
                 K.gpf_g = 8;
             }
-            const char *ge = getenv("PBGPU_G");
-            if (ge && (atoi(ge) == 8 || atoi(ge) == 16 || atoi(ge) == 32 || atoi(ge) == 64))
-                K.gpf_g = (uint32_t)atoi(ge);
+            if (O.g)
+                K.gpf_g = O.g;
             K.gpf_rmode = n_random == (int)pls.size() ? 1 : (n_random == 0 ? 0 : 2);
             const uint32_t ngw = PB_WG / K.gpf_g; // frames in flight per workgroup
-            uint32_t fpw = PB_WG;
-            const char *fe = getenv("PBGPU_FPW");
-            if (fe && atoi(fe) > 0)
-                fpw = (uint32_t)atoi(fe);
+            uint32_t fpw = O.fpw ? O.fpw : PB_WG;
             fpw = fpw < ngw ? ngw : (fpw > PB_WG ? PB_WG : fpw);
             K.gpf_fpw = fpw / ngw * ngw;
 
@@ -1038,7 +1119,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             // unmasked); PBGPU_KERNEL=gpf forces the group-per-frame kernel.  A flat B
             // (one list of the window's payload chunks, checksums from LCG-cycle prefix
             // sums) measured slower: 2.1-2.5 ms
-            const bool gpf_only = kern && !strcmp(kern, "gpf");
+            const bool gpf_only = O.kernel == PBO_K_GPF;
             const uint32_t avg = (minf + maxf) / 2;
             const uint32_t npc = (avg - K.hl) / 16 + 2;
             double umax = 0;
@@ -1053,25 +1134,22 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 }
             if (!K.fixed_len)
                 sg = 8;
-            if (ge && (atoi(ge) == 8 || atoi(ge) == 16 || atoi(ge) == 32 || atoi(ge) == 64))
-                sg = (uint32_t)atoi(ge);
-            uint32_t wgt = PB_WG;
-            if (const char *e = getenv("PBGPU_WGT"))
-                wgt = atoi(e) == 64 ? 64 : PB_WG;
+            if (O.g)
+                sg = O.g;
+            const uint32_t wgt = O.wgt == 64 ? 64u : (uint32_t)PB_WG;
             uint32_t wgf = K.fixed_len ? 64 : 128;
-            if (const char *e = getenv("PBGPU_WGF"))
-                wgf = atoi(e) > 0 && atoi(e) <= PB_WG ? (uint32_t)atoi(e) : wgf;
+            if (O.wgf && O.wgf <= PB_WG)
+                wgf = O.wgf;
             wgf = std::min(wgf, wgt);
-            const char *ekb = getenv("PBGPU_STAGE_KB");
             uint32_t win, sbytes;
             if (K.fixed_len)
             {
                 const uint32_t ngw2 = std::max(1u, wgt / sg);
                 uint32_t fw = ngw2 * std::max(1u, (20u * 1024 * wgt / PB_WG) / (ngw2 * maxf));
-                if (ekb && atoi(ekb) > 0)
-                    fw = std::max(1u, (uint32_t)atoi(ekb) * 1024 / maxf);
-                if (fe && atoi(fe) > 0)
-                    fw = (uint32_t)atoi(fe);
+                if (O.stage_kb)
+                    fw = std::max(1u, O.stage_kb * 1024 / maxf);
+                if (O.fpw)
+                    fw = O.fpw;
                 const uint32_t fit = (uint32_t)((64 * 1024 - 48 - PB_STAGE_LDS(std::max(wgf, fw))) / maxf);
                 fw = std::max(1u, std::min(fw, fit)); // the stage must fit 64 KiB of LDS
                 win = fw * maxf;
@@ -1082,7 +1160,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 // 24 KiB windows.  pb_vstage_kernel (configs[2], 2^25 frames, profiles/r02/ab/hv2_*):
                 // 6.37 ms at 24 KiB, 6.68 at 16, 7.34 at 28 (3 workgroups per CU) since it keeps
                 // only 9 header dwords per frame in LDS; with 16-dword images 16 KiB was best
-                const uint32_t skb = ekb && atoi(ekb) > 0 ? (uint32_t)atoi(ekb) : 24;
+                const uint32_t skb = O.stage_kb ? O.stage_kb : 24;
                 sbytes = (skb * 1024 + 15) / 16 * 16;
                 if (sbytes < 2 * maxf + 48)
                     sbytes = (2 * maxf + 48 + 15) / 16 * 16;
@@ -1093,7 +1171,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 const uint32_t fw = win / maxf; // whole windows per workgroup
                 wgf = fw > wgt ? wgt : std::min<uint32_t>(wgt / fw * fw, fw * ((wgf + fw - 1) / fw));
             }
-            else if (!getenv("PBGPU_WGF"))
+            else if (!O.wgf)
                 wgf = std::min<uint32_t>(wgt, std::max(wgf, win / minf + 1));
             if (!gpf_only && sbytes + PB_STAGE_LDS(wgf) <= 64 * 1024)
             {
@@ -1105,18 +1183,18 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 // every payload random, stream rule: pb_vstage_kernel (no header pass, no
                 // serial byte loops in phase A; configs[2] 1.74 vs 1.87 ms per 2^23 frames at
                 // the best window of each); PBGPU_KERNEL=stage keeps pb_stage_kernel
-                if (K.gpf_rmode == 1 && !(flags & PBK_LITERAL) && wgt == PB_WG && !env_is("PBGPU_KERNEL", "stage") &&
+                if (K.gpf_rmode == 1 && !(flags & PBK_LITERAL) && wgt == PB_WG && O.kernel != PBO_K_STAGE &&
                     sbytes + PB_VST_LDS(wgf) <= 64 * 1024)
                 {
                     K.vst = 1;
-                    K.fst_dbg = (uint32_t)env_int("PBGPU_FST_DBG", 0);
+                    K.vst_shape = O.vst_shape;
                     // phase A has one lane per slot (ghosts + own frames): as many own frames as
                     // lanes allow, which also spreads the per-workgroup work over the most windows
                     // (configs[2], 2^25 frames: 6.37 ms at 240-252 vs 6.44 at 218 and 6.50 at 200;
                     // profiles/r02/ab/wf24*)
                     // (as many as still leave 4 workgroups per CU when the window's frames fit)
                     K.stage_wgf = std::min<uint32_t>(K.stage_wgf, PB_WG - PB_VST_GHOSTS);
-                    if (!getenv("PBGPU_WGF") && !K.fixed_len)
+                    if (!O.wgf && !K.fixed_len)
                     {
                         uint32_t best = PB_WG - PB_VST_GHOSTS;
                         while (best > K.stage_wgf && K.stage_bytes + PB_VST_LDS(best) > 160 * 1024 / 4)
@@ -1134,17 +1212,17 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             // pb_stage_kernel 2.29.  PBGPU_KERNEL=stage / gpf keep the older kernels,
             // PBGPU_FST_G, PBGPU_FST_WGF, PBGPU_FST_NBUF override the shape.
             const bool fst_ok = K.fixed_len && minf > 128 && minf % 4 == 0 && K.gpf_rmode == 1 &&
-                                !(flags & PBK_LITERAL) && !gpf_only && !env_is("PBGPU_KERNEL", "stage");
+                                !(flags & PBK_LITERAL) && !gpf_only && O.kernel != PBO_K_STAGE;
             // packed variable lengths, every payload random, stream rule, payloads of >= 32 B:
             // pb_vline_kernel (no LDS stage).  ICMP type 0 / code 0 is left to
             // pb_vstage_kernel: its header word sum can be 0, where the orbit sums cannot tell a
             // zero payload sum from 0xFFFF.  PBGPU_KERNEL=vstage keeps pb_vstage_kernel.
             const bool icmp00 = proto == 1 && t[34] == 0 && t[35] == 0;
             if (!K.fixed_len && K.gpf_rmode == 1 && !(flags & PBK_LITERAL) && !gpf_only && minf >= K.hl + 32 &&
-                maxf <= 4096 && !icmp00 && !env_is("PBGPU_KERNEL", "vstage") && !env_is("PBGPU_KERNEL", "stage"))
+                maxf <= 4096 && !icmp00 && O.kernel != PBO_K_VSTAGE && O.kernel != PBO_K_STAGE)
             {
                 const uint32_t nsp = K.hl == 54 ? 5u : 4u;
-                uint32_t wf = (uint32_t)env_int("PBGPU_VL_WGF", PB_WG - PB_VST_GHOSTS);
+                uint32_t wf = O.vl_wgf ? O.vl_wgf : PB_WG - PB_VST_GHOSTS;
                 wf = std::max(32u, std::min<uint32_t>(wf, PB_WG - PB_VST_GHOSTS));
                 uint32_t nl48 = 0, nlines = 0;
                 for (;; wf -= 4)
@@ -1173,13 +1251,10 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 K.vl_nlines = nlines;
                 K.orbit = ctx->d_orbit;
                 K.orbit_tot = ctx->orbit_tot;
-                K.fst_dbg = (uint32_t)env_int("PBGPU_FST_DBG", 0);
             }
             if (fst_ok)
             {
-                const uint32_t eg = (uint32_t)env_int("PBGPU_FST_G", 0);
-                const uint32_t ew = (uint32_t)env_int("PBGPU_FST_WGF", 0);
-                const uint32_t en = (uint32_t)env_int("PBGPU_FST_NBUF", 0);
+                const uint32_t eg = O.fst_g, ew = O.fst_wgf, en = O.fst_nbuf;
                 for (uint32_t nb : {1u, 2u})
                 {
                     if (en && nb != en)
@@ -1198,7 +1273,6 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                             K.fst_wgf = fw;
                             K.fst_sb = sb;
                             K.fst_nbuf = nb;
-                            K.fst_dbg = (uint32_t)env_int("PBGPU_FST_DBG", 0);
                             break;
                         }
                     }
@@ -1225,8 +1299,8 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     K.jump = ctx->d_jump;
     K.lcg48 = ctx->d_lcg48;
     K.counters = ctx->d_counters + PB_CTR_WORDS * seq_idx;
-    K.lds_pad = (uint32_t)env_int("PBGPU_LDS_PAD", (int)K.lds_pad);
     S.K = K;
+    S.opt = O;
     S.loaded = true;
     return PBGPU_OK;
 }
@@ -1256,9 +1330,7 @@ int pbgpu_frames_alloc(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capaci
         return PBGPU_ENOMEM;
     capacity_bytes = (capacity_bytes + 15) & ~15ull;
     // +64 B: word-granular readers (UMEM scatter) may touch a few bytes past the last frame
-    // (experiments) PBGPU_ALLOC_CONTIG=1: physically contiguous frame memory
-    const unsigned alloc_flags = env_is("PBGPU_ALLOC_CONTIG", "1") ? hipDeviceMallocContiguous : hipDeviceMallocDefault;
-    if (hipExtMallocWithFlags((void **)&f->data, capacity_bytes + 64, alloc_flags) != hipSuccess ||
+    if (hipMalloc((void **)&f->data, capacity_bytes + 64) != hipSuccess ||
         hipMalloc((void **)&f->offsets, (capacity_frames + 1) * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc((void **)&f->scan_tmp, scan_tmp_bytes(capacity_frames)) != hipSuccess)
     {
@@ -1321,95 +1393,6 @@ static int timed_pair(pbgpu_ctx *ctx, timing_pair *p)
     return PBGPU_OK;
 }
 
-// One batch of the hot loop, sequence.c:433-602.
-// Diagnostic (PBGPU_TIMING with a -DPB_TIMING=1 build): mean phase durations of
-// the staged kernel's workgroups and the mean number of resident workgroups.
-static void report_phase_timing(pbgpu_ctx *ctx, uint64_t n_wg)
-{
-    std::vector<unsigned long long> h(n_wg * 8);
-    if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
-        hipMemcpy(h.data(), ctx->d_dbg, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
-        return;
-    double ph[4] = {0, 0, 0, 0}, life = 0;
-    unsigned long long t0 = ~0ull, t1 = 0;
-    uint64_t n = 0;
-    for (uint64_t w = 0; w < n_wg; ++w)
-    {
-        const unsigned long long *r = &h[w * 8];
-        if (!r[0] || !r[6])
-            continue;
-        ++n;
-        for (int i = 0; i < 4; ++i)
-            ph[i] += (double)r[i + 1];
-        life += (double)(r[6] - r[0]);
-        t0 = r[0] < t0 ? r[0] : t0;
-        t1 = r[6] > t1 ? r[6] : t1;
-    }
-    if (!n)
-        return;
-    fprintf(stderr,
-            "{\"pbgpu_timing\": {\"workgroups\": %llu, \"cycles_A\": %.0f, \"cycles_B_sum\": %.0f, \"cycles_C_sum\": %.0f, "
-            "\"cycles_S_sum\": %.0f, \"life_us\": %.3f, \"span_us\": %.3f, \"resident_wg\": %.1f}}\n",
-            (unsigned long long)n, ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, life / n / 100.0, (t1 - t0) / 100.0,
-            life / (double)(t1 - t0));
-}
-
-// pb_xsmall_kernel's occupancy, chosen per frame buffer.  With non-temporal stores the 64-B page
-// kernel capped at 5 workgroups per CU runs 0.309-0.311 ms per 2^25 frames in some buffers and
-// 0.35-0.36 in others, where the uncapped shape runs 0.33 in all (profiles/r04/ab/ab17_*, ab18_*:
-// the cap's rate depends on the buffer's placement, as the region kernels' do).
-// So the first build of >= 2^22 64-B frames into a buffer times both shapes on it (after a
-// warm-up, 3 alternating rounds of 20 launches: the same frames; count records into a scratch
-// array) and keeps the cap for that buffer if it is >= 1% faster.  Synchronous, once per buffer
-// (~0.07 s at 2^25 frames); PBGPU_XS_TUNE=0 skips it (uncapped), PBGPU_LDS_PAD overrides it.
-#define PB_XS_TUNE_PAD (32768u - 4u * PB_XREG) // 17-KiB tile + pad = 32 KiB: 5 workgroups per CU
-static int tune_xsmall(pbgpu_ctx *ctx, const pb_kargs &K, hipStream_t st, int *xs_pad)
-{
-    pb_kargs T = K;
-    if (ctx->d_tune_slots == nullptr || ctx->tune_cap < T.xs_grid)
-    {
-        if (ctx->d_tune_slots)
-            (void)hipFree(ctx->d_tune_slots);
-        ctx->d_tune_slots = nullptr;
-        ctx->tune_cap = 0;
-        HIPCHK(hipMalloc((void **)&ctx->d_tune_slots, (size_t)T.xs_grid * sizeof(uint32_t)));
-        ctx->tune_cap = T.xs_grid;
-    }
-    T.ctr_slots = ctx->d_tune_slots;
-    hipEvent_t a, b;
-    HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
-    const uint32_t pads[2] = {0u, PB_XS_TUNE_PAD};
-    double best[2] = {1e30, 1e30};
-    hipError_t e = hipSuccess;
-    // 80 untimed launches bring the clocks up (the first ~60 ms of a run are slower), then three
-    // rounds of 20 back-to-back launches per shape (the cap's effect shows under sustained load)
-    for (int i = 0; i < 80 && e == hipSuccess; ++i)
-        e = pbk_launch_build(&T, st);
-    for (int r = 0; r < 3 && e == hipSuccess; ++r)
-        for (int v = 0; v < 2 && e == hipSuccess; ++v)
-        {
-            T.lds_pad = pads[v];
-            e = hipEventRecord(a, st);
-            for (int i = 0; i < 20 && e == hipSuccess; ++i)
-                e = pbk_launch_build(&T, st);
-            if (e == hipSuccess)
-                e = hipEventRecord(b, st);
-            if (e == hipSuccess)
-                e = hipEventSynchronize(b);
-            float ms = 0.f;
-            if (e == hipSuccess)
-                e = hipEventElapsedTime(&ms, a, b);
-            if (e == hipSuccess)
-                best[v] = ms / 20 < best[v] ? ms / 20 : best[v];
-        }
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
-    HIPCHK(e);
-    *xs_pad = best[1] < 0.99 * best[0] ? (int)pads[1] : 0;
-    return PBGPU_OK;
-}
-
 // The frames' build-completion event (kept in pbgpu_frames.reserved): the
 // landing stream waits on it, so landing one buffer overlaps building the next.
 static int mark_built(pbgpu_ctx *ctx, pbgpu_frames *out, hipStream_t st)
@@ -1459,18 +1442,19 @@ struct batch_part
     uint32_t wgt;
     pb_kargs K;
     bool built;
+    uint64_t ctr_words; // count-ring words the part reserved (returned if the launch fails)
 };
 
-// pbgpu_build, or with bp: every step of it but the launch (and its timing), on bp->st
-static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, pbgpu_frames *out,
-                      batch_part *bp)
+// Every argument check of a build, before anything is changed (pbgpu_build_batch checks all its
+// parts first, so a part that cannot be built leaves the others untouched).
+static int build_check(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter,
+                       const pbgpu_frames *out)
 {
     if (ctx == NULL || out == NULL || seq_idx >= PB_MAX_SEQUENCES)
         return PBGPU_EINVAL;
-    seq_slot &S = ctx->seqs[seq_idx];
+    const seq_slot &S = ctx->seqs[seq_idx];
     if (!S.loaded)
         return PBGPU_ENOENT;
-    HIPCHK(hipSetDevice(ctx->device));
     const uint64_t nf = n_iter * S.fpi;
     if (nf > out->capacity_frames || nf > 0xFFFFFFFFull)
         return PBGPU_ENOSPC;
@@ -1479,6 +1463,21 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
     const uint64_t max_bytes = nf * S.max_flen;
     if (((max_bytes + 15) & ~15ull) > out->capacity_bytes)
         return PBGPU_ENOSPC;
+    return PBGPU_OK;
+}
+
+// pbgpu_build, or with bp: every step of it but the launch (and its timing), on bp->st
+static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t n_iter, pbgpu_frames *out,
+                      batch_part *bp)
+{
+    {
+        const int crc = build_check(ctx, seq_idx, first_iter, n_iter, out);
+        if (crc != PBGPU_OK)
+            return crc;
+    }
+    seq_slot &S = ctx->seqs[seq_idx];
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint64_t nf = n_iter * S.fpi;
 
     // the stream this build runs on: the sequence's own in span mode (builds of different
     // sequences overlap), the context's otherwise (each launch timed on its own)
@@ -1487,7 +1486,7 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
     int si = -1;
     if (bp)
         st = bp->st, bp->built = false;
-    else if (span && !env_is("PBGPU_SEQ_STREAMS", "0"))
+    else if (span && ctx->opt.seq_streams)
     {
         si = seq_idx % PB_SEQ_STREAMS;
         if (ctx->seq_stream[si] == nullptr)
@@ -1514,8 +1513,6 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
         fe->land_pending = false;
     }
     pb_kargs K = S.K;
-    K.xcd_rot = (uint32_t)env_int("PBGPU_XCD_ROT", 0); // (experiments) pb_xcd_region rotation
-    K.store_flip = env_is("PBGPU_STORE_FLIP", "1") ? 1u : 0u;
     K.first_iter = first_iter;
     K.n_frames = nf;
     K.out = out->data;
@@ -1541,7 +1538,7 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
         K.vblk_l2 = nullptr;
         K.offsets_w = nullptr;
         const uint32_t wgf = K.vl ? K.vl_wgf : K.stage_wgf;
-        if (K.vl || (K.vst && K.stage_wgf >= PB_VST_SCAN_MIN_WGF && !env_is("PBGPU_VST_SCAN", "3pass")))
+        if (K.vl || (K.vst && K.stage_wgf >= PB_VST_SCAN_MIN_WGF && !S.opt.vst_scan3))
         {
             // pb_vline_kernel / pb_vstage_kernel: per-workgroup length sums, their scan, offsets
             // written by the build
@@ -1576,31 +1573,41 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
         }
     }
     K.xs_grid = 0;
-    if (bp && K.small_ndw && K.xs_np && !K.xp) // pb_xsmall_body at the batch's block size
+    if (bp && K.small_ndw && K.xs_np && !K.xp) // pb_batch_kernel's 64-B part at the batch's block size
         K.xs_np = bp->wgt >> K.xs_fp_shift;
-    if (K.small_ndw && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && !env_is("PBGPU_KERNEL", "linear"))
+    if (K.small_ndw && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && S.opt.kernel != PBO_K_LINEAR)
     {
-        // XCD-owned 4 KiB pages (pb_xsmall_kernel): groups of 8 workgroups x 4 pages, tail pages in order
+        // XCD-owned 4 KiB pages, xs_np per workgroup: pb_xsmall_kernel (one wave per page) takes
+        // groups of 8 workgroups (pages past the stream are skipped); pb_xpage_kernel and the
+        // batch's 64-B part take full groups of 8, then the tail pages in order
         const uint64_t nch = (K.total_bytes + 4095) / 4096;
         if (nch < 0x7FFFFFFFull)
         {
             K.xs_nch = (uint32_t)nch;
             const uint32_t np = K.xs_np;
             K.xs_full = (uint32_t)(nch / (8 * np) * 8);
-            K.xs_grid = K.xs_full + (uint32_t)((nch - (uint64_t)K.xs_full * np + np - 1) / np);
+            if (K.xp || bp)
+                K.xs_grid = K.xs_full + (uint32_t)((nch - (uint64_t)K.xs_full * np + np - 1) / np);
+            else
+                K.xs_grid = (uint32_t)((nch + 8ull * np - 1) / (8ull * np) * 8);
             // (PBGPU_XP_FA64=1: the 64-bit path at any size, so the tests reach it)
-            K.xp_fa_hi = K.xp && ((uint64_t)nch * (4096 % K.fixed_len) >= (1ull << 31) || env_is("PBGPU_XP_FA64", "1"));
+            K.xp_fa_hi = K.xp && ((uint64_t)nch * (4096 % K.fixed_len) >= (1ull << 31) || S.opt.xp_fa64);
         }
     }
+    timing_pair tp = {nullptr, nullptr};
+    int rc = PBGPU_OK;
+    if (!bp && !span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
+        return rc;
     // this launch's per-workgroup count records (pb_count): the next words of the sequence's
     // ring, folded into the counters first when it is full (PBGPU_CTR_ATOMIC=1: one atomic per
-    // workgroup instead)
-    int rc = PBGPU_OK;
+    // workgroup instead).  Reserved last, after everything that can fail but the launch itself;
+    // a launch that fails returns them (its records would never be written)
     K.ctr_slots = nullptr;
-    if (!env_is("PBGPU_CTR_ATOMIC", "1"))
+    uint64_t words = 0;
+    if (!S.opt.ctr_atomic)
     {
         const uint64_t pairs = K.fixed_len ? 1 : 2;
-        const uint64_t words = (uint64_t)pbk_build_grid(&K) * pairs;
+        words = (uint64_t)pbk_build_grid(&K) * pairs;
         if (S.ctr_pairs != pairs || S.ctr_used + words > S.ctr_cap)
         {
             if ((rc = ctr_fold(ctx, seq_idx, st)) != PBGPU_OK)
@@ -1614,8 +1621,7 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
                 S.d_ctr_slots = nullptr;
                 S.ctr_cap = 0;
                 // (PBGPU_CTR_RING = words: a small ring, so the tests reach the fold-when-full path)
-                const int er = env_int("PBGPU_CTR_RING", 0);
-                const uint64_t ring = er > 0 ? (uint64_t)er : PB_CTR_RING_WORDS;
+                const uint64_t ring = S.opt.ctr_ring ? (uint64_t)S.opt.ctr_ring : PB_CTR_RING_WORDS;
                 const uint64_t cap = words > ring ? words : ring;
                 HIPCHK(hipMalloc((void **)&S.d_ctr_slots, cap * sizeof(uint32_t)));
                 S.ctr_cap = cap;
@@ -1630,37 +1636,10 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
     {
         bp->K = K;
         bp->built = true;
+        bp->ctr_words = words;
         return PBGPU_OK;
     }
-    // pb_xsmall_kernel: the occupancy measured on this buffer (tune_xsmall)
-    if (K.small_ndw == 16 && K.xs_grid && !K.xp && K.lds_pad == 0 && getenv("PBGPU_LDS_PAD") == NULL &&
-        !env_is("PBGPU_XS_TUNE", "0"))
-    {
-        if (fe->xs_pad < 0 && nf >= (1u << 22) && (rc = tune_xsmall(ctx, K, st, &fe->xs_pad)) != PBGPU_OK)
-            return rc;
-        if (fe->xs_pad > 0)
-            K.lds_pad = (uint32_t)fe->xs_pad;
-        ctx->xs_tuned_last = fe->xs_pad;
-    }
-    timing_pair tp = {nullptr, nullptr};
-    if (!span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
-        return rc;
-    const bool timing = (K.stage_win || K.fst_g) && getenv("PBGPU_TIMING") != NULL; // diagnostic builds (PB_TIMING)
-    const uint32_t wg_frames = K.fst_g ? K.fst_wgf : K.stage_wgf;
-    const uint64_t n_wg = wg_frames ? (nf + wg_frames - 1) / wg_frames : 0;
-    if (timing)
-    {
-        if (ctx->dbg_cap < n_wg)
-        {
-            if (ctx->d_dbg)
-                (void)hipFree(ctx->d_dbg);
-            ctx->d_dbg = nullptr;
-            HIPCHK(hipMalloc((void **)&ctx->d_dbg, n_wg * 8 * sizeof(unsigned long long)));
-            ctx->dbg_cap = n_wg;
-        }
-        HIPCHK(hipMemsetAsync(ctx->d_dbg, 0, n_wg * 8 * sizeof(unsigned long long), st));
-        K.dbg = ctx->d_dbg;
-    }
+    hipError_t le = hipSuccess;
     if (span)
     {
         if (ctx->span_n == 0)
@@ -1683,17 +1662,26 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
             }
             ctx->seq_dirty[si] = true;
         }
-        HIPCHK(pbk_launch_build(&K, st));
+        le = pbk_launch_build(&K, st);
+        if (le != hipSuccess)
+        {
+            S.ctr_used -= words;
+            HIPCHK(le);
+        }
         ++ctx->span_n;
         return mark_built(ctx, out, st);
     }
     HIPCHK(hipEventRecord(tp.a, ctx->stream));
-    HIPCHK(pbk_launch_build(&K, ctx->stream));
+    le = pbk_launch_build(&K, ctx->stream);
+    if (le != hipSuccess)
+    {
+        S.ctr_used -= words;
+        ctx->pool.push_back(tp);
+        HIPCHK(le);
+    }
     HIPCHK(hipEventRecord(tp.b, ctx->stream));
     if ((rc = mark_built(ctx, out, st)) != PBGPU_OK)
         return rc;
-    if (timing)
-        report_phase_timing(ctx, n_wg);
     ctx->pending.push_back(tp);
     if (ctx->pending.size() >= 4096)
     {
@@ -1711,24 +1699,21 @@ int pbgpu_build(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uint64_t 
     return build_impl(ctx, seq_idx, first_iter, n_iter, out, nullptr);
 }
 
-// pb_batch_kernel's block size (PBGPU_BATCH_WGT=256: the 256-thread form)
-static uint32_t batch_wgt()
-{
-    return env_int("PBGPU_BATCH_WGT", 512) == 256 ? 256u : 512u;
-}
 
 // The fused form applies: three distinct sequences of kinds 1, 2, 3 (pbk_batch_kind), into three
 // distinct 4-KiB-aligned buffers, each with frames to build; order[k] = the part of kind k + 1
 static bool batch_fusable(pbgpu_ctx *ctx, uint32_t n, const uint16_t *seq_idx, const uint64_t *n_iter,
                           pbgpu_frames *const *outs, uint32_t order[3])
 {
-    if (n != 3 || env_is("PBGPU_BATCH", "0") || env_is("PBGPU_KERNEL", "linear"))
+    if (n != 3)
         return false;
     bool seen[3] = {false, false, false};
     for (uint32_t i = 0; i < 3; ++i)
     {
         const seq_slot &S = ctx->seqs[seq_idx[i]];
-        const int kd = S.loaded ? pbk_batch_kind(&S.K) : 0;
+        if (!S.loaded || !S.opt.batch || S.opt.kernel == PBO_K_LINEAR)
+            return false;
+        const int kd = pbk_batch_kind(&S.K);
         if (kd < 1 || kd > 3 || seen[kd - 1] || n_iter[i] == 0 || ((uintptr_t)outs[i]->data & 4095u) != 0)
             return false;
         seen[kd - 1] = true;
@@ -1748,6 +1733,14 @@ int pbgpu_build_batch(pbgpu_ctx *ctx, uint32_t n, const uint16_t *seq_idx, const
     for (uint32_t i = 0; i < n; ++i)
         if (outs[i] == NULL || seq_idx[i] >= PB_MAX_SEQUENCES)
             return PBGPU_EINVAL;
+    // every part's arguments first: a part that cannot be built fails the call before any part
+    // is launched or reserves count records
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        const int rc = build_check(ctx, seq_idx[i], first_iter[i], n_iter[i], outs[i]);
+        if (rc != PBGPU_OK)
+            return rc;
+    }
     HIPCHK(hipSetDevice(ctx->device));
     uint32_t order[3];
     if (!batch_fusable(ctx, n, seq_idx, n_iter, outs, order))
@@ -1764,44 +1757,59 @@ int pbgpu_build_batch(pbgpu_ctx *ctx, uint32_t n, const uint16_t *seq_idx, const
     // every part on the context's stream, then one launch
     hipStream_t st = ctx->stream;
     const bool span = ctx->timing_mode == PBGPU_TIMING_SPAN;
+    timing_pair tp = {nullptr, nullptr};
+    if (!span)
+    {
+        const int rc = timed_pair(ctx, &tp);
+        if (rc != PBGPU_OK)
+            return rc;
+    }
     batch_part bp[3]; // (build_impl orders each part after its buffer's and count ring's last stream)
     pb_kargs Ks[3];
+    // a failure after parts reserved count records returns them (those records are never written)
+    auto unreserve = [&](uint32_t parts) {
+        for (uint32_t k = 0; k < parts; ++k)
+            ctx->seqs[seq_idx[order[k]]].ctr_used -= bp[k].ctr_words;
+        if (tp.a)
+            ctx->pool.push_back(tp);
+    };
     for (uint32_t k = 0; k < 3; ++k)
     {
         const uint32_t i = order[k];
         bp[k].st = st;
-        bp[k].wgt = batch_wgt();
+        bp[k].wgt = ctx->opt.batch_wgt;
+        bp[k].ctr_words = 0;
         const int rc = build_impl(ctx, seq_idx[i], first_iter[i], n_iter[i], outs[i], &bp[k]);
-        if (rc != PBGPU_OK)
-            return rc;
-        if (!bp[k].built)
-            return PBGPU_EINVAL; // (n_iter > 0 was checked: unreachable)
+        if (rc != PBGPU_OK || !bp[k].built)
+        {
+            unreserve(k + (rc == PBGPU_OK ? 1u : 0u));
+            return rc != PBGPU_OK ? rc : PBGPU_EINVAL; // (n_iter > 0 was checked: not built is unreachable)
+        }
         Ks[k] = bp[k].K;
     }
-    if (span)
+    if (span && ctx->span_n == 0)
     {
-        if (ctx->span_n == 0)
+        if (ctx->span.a == nullptr)
         {
-            if (ctx->span.a == nullptr)
-            {
-                HIPCHK(hipEventCreate(&ctx->span.a));
-                HIPCHK(hipEventCreate(&ctx->span.b));
-            }
-            HIPCHK(hipEventRecord(ctx->span.a, ctx->stream));
-            for (bool &j : ctx->seq_in_span)
-                j = false;
+            HIPCHK(hipEventCreate(&ctx->span.a));
+            HIPCHK(hipEventCreate(&ctx->span.b));
         }
-        HIPCHK(pbk_launch_batch(Ks, batch_wgt(), st));
-        ++ctx->span_n;
+        HIPCHK(hipEventRecord(ctx->span.a, ctx->stream));
+        for (bool &j : ctx->seq_in_span)
+            j = false;
     }
+    if (!span)
+        HIPCHK(hipEventRecord(tp.a, st));
+    const hipError_t le = pbk_launch_batch(Ks, ctx->opt.batch_wgt, st);
+    if (le != hipSuccess)
+    {
+        unreserve(3);
+        HIPCHK(le);
+    }
+    if (span)
+        ++ctx->span_n;
     else
     {
-        timing_pair tp = {nullptr, nullptr};
-        int rc = timed_pair(ctx, &tp);
-        if (rc != PBGPU_OK)
-            return rc;
-        HIPCHK(hipEventRecord(tp.a, st));
-        HIPCHK(pbk_launch_batch(Ks, batch_wgt(), st));
         HIPCHK(hipEventRecord(tp.b, st));
         ctx->pending.push_back(tp);
     }
@@ -1913,7 +1921,7 @@ int pbgpu_host_unregister(pbgpu_ctx *ctx, void *ptr)
 // device address of [p, p + n) in a registered (mapped) range, or NULL
 static uint8_t *mapped(pbgpu_ctx *ctx, uint8_t *p, uint64_t n)
 {
-    if (getenv("PBGPU_UMEM_DMA"))
+    if (ctx->opt.umem_dma)
         return NULL;
     for (const auto &r : ctx->regs)
         if (p >= r.host && p + n <= r.host + r.bytes)
@@ -1961,7 +1969,7 @@ int pbgpu_land_wait(pbgpu_ctx *ctx, uint32_t keep)
         // a sender waits on every landing: poll the event rather than block in the runtime
         // (a blocking wait adds its wake-up latency to each landing; PBGPU_LAND_SPIN=0 blocks)
         hipError_t e = hipSuccess;
-        if (ctx->land_spin)
+        if (ctx->opt.land_spin)
             e = spin_wait(op.ev);
         else
             e = hipEventSynchronize(op.ev);
@@ -2355,12 +2363,12 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
-    else if (K.xs_np && K.xp && !env_is("PBGPU_KERNEL", "linear"))
+    else if (K.xs_np && K.xp && S.opt.kernel != PBO_K_LINEAR)
         snprintf(buf, n, "pb_xpage_kernel<%u, %u, %s, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
                  K.xp_wgt, K.fixed_len % 4 == 0 ? "true" : "false");
-    else if (K.xs_np && !env_is("PBGPU_KERNEL", "linear"))
-        snprintf(buf, n, "pb_xsmall_kernel<%u, %u, %s, %u>%s", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
-                 (uint32_t)PB_WG, ctx->xs_tuned_last > 0 && K.small_ndw == 16 ? " (5 wg/CU, tuned)" : "");
+    else if (K.xs_np && S.opt.kernel != PBO_K_LINEAR)
+        snprintf(buf, n, "pb_xsmall_kernel<%u, %u, %s, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
+                 (uint32_t)PB_WG);
     else
         snprintf(buf, n, "pb_small_kernel<%u, %u, %s, %u, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
                  K.small_wgt ? K.small_wgt : (uint32_t)PB_WG, K.fixed_len % 4 == 2 ? 2u : 0u);

@@ -149,70 +149,17 @@ __device__ __forceinline__ uint32_t pb_bytemask(int lo, int hi, int t)
     return ge & lt;
 }
 
-// 16-B output store.  The store kind is fixed at compile time (PB_NT): a
-// runtime choice between a non-temporal and a plain store gets merged into one
-// plain store by the compiler, dropping the non-temporal bit.
-#ifndef PB_NT
-#define PB_NT 0
-#endif
+// 16-B output stores, plain and non-temporal.  Each kernel has one kind, fixed in its code (a
+// run-time choice between the two gets merged into one plain store by the compiler).  Measured
+// per kernel: non-temporal for the page kernels, pb_small_kernel and
+// pb_vline_kernel; plain for pb_fstage_kernel and the staged kernels.
 __device__ __forceinline__ void pb_st16(uint8_t *p, pb_u32x4 v)
 {
-#if PB_NT
-    __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
-#else
     *reinterpret_cast<pb_u32x4 *>(p) = v;
-#endif
 }
-#ifndef PB_SMALL_DYN
-#define PB_SMALL_DYN 1 // pb_small_kernel's LDS tile sized to its frames (dynamic) instead of WGT * NDW dwords
-#endif
-#ifndef PB_SX_NT
-#define PB_SX_NT 1 // pb_small_kernel's and pb_xpage_kernel's stores are non-temporal
-#endif
-#ifndef PB_FS_NT
-#define PB_FS_NT 0 // pb_fstage_kernel's stores non-temporal (its template default; PBGPU_STORE_FLIP=1 the other kind)
-#endif
-#ifndef PB_XS_NT
-// pb_xsmall_kernel's stores non-temporal (round 4: 0.333 vs 0.344 ms, 0.334 vs 0.344, 0.342 vs
-// 0.356 and 0.3325 vs 0.3287 per 2^25 64-B frames on four boxes, profiles/r04/ab/ab12-13_*;
-// plain stores had won in round 3, when each workgroup still added its counts with atomics)
-#define PB_XS_NT 1
-#endif
-__device__ __forceinline__ void pb_st16_xs(uint8_t *p, pb_u32x4 v)
+__device__ __forceinline__ void pb_st16_nt(uint8_t *p, pb_u32x4 v)
 {
-#if PB_XS_NT
     __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
-#else
-    pb_st16(p, v);
-#endif
-}
-__device__ __forceinline__ void pb_st16_sx(uint8_t *p, pb_u32x4 v)
-{
-#if PB_SX_NT
-    __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
-#else
-    pb_st16(p, v);
-#endif
-}
-#ifndef PB_VL_NT
-#define PB_VL_NT 1 // pb_vline_kernel's frame stores are non-temporal
-#endif
-// NT: the store kind as a template parameter (each kernel instance keeps one kind)
-template <bool NT>
-__device__ __forceinline__ void pb_st16_k(uint8_t *p, pb_u32x4 v)
-{
-    if (NT)
-        __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
-    else
-        *reinterpret_cast<pb_u32x4 *>(p) = v;
-}
-__device__ __forceinline__ void pb_st16_vl(uint8_t *p, pb_u32x4 v)
-{
-#if PB_VL_NT
-    __builtin_nontemporal_store(v, reinterpret_cast<pb_u32x4 *>(p));
-#else
-    pb_st16(p, v);
-#endif
 }
 
 // 4 payload bytes from 4 consecutive LCG states: byte = state[23:16]
@@ -332,19 +279,12 @@ constexpr uint32_t PB_C3 = PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u);
 // frames) taken by workgroup b: XCD x builds the x-th contiguous eighth of the regions, in
 // order, instead of every eighth region (the rest, fewer than 8, keep their own index).
 // Measured on the 1500-B staged kernel: 7.17 vs 8.45 ms per 2^25 frames.
-// rot > 0 (experiments): XCD x starts its walk (x * rot * per / 256) regions into its eighth and
-// wraps, so the eight write fronts are per + rot * per / 256 regions apart instead of per.
-__device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg, uint32_t rot = 0)
+__device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg)
 {
     const uint32_t per = nwg >> 3;
     if (b >= 8u * per)
         return b;
-    const uint32_t x = b & 7u, j = b >> 3;
-    if (rot == 0)
-        return x * per + j;
-    const uint32_t o = (uint32_t)(((uint64_t)per * rot * x) >> 8) % per;
-    const uint32_t jj = j + o;
-    return x * per + (jj >= per ? jj - per : jj);
+    return (b & 7u) * per + (b >> 3);
 }
 
 // The reference's total_pckts / total_bytes (sequence.c:633-642), counted as work is done: each
@@ -356,15 +296,10 @@ __device__ __forceinline__ uint32_t pb_xcd_region(uint32_t b, uint32_t nwg, uint
 // counters.  A device-scope atomic per workgroup instead executes at the memory side as its own
 // 64-B request: 0.4% of a 64-B launch's HBM traffic (profiles/pmc_r03.json).  Without a slot array
 // (K.ctr_slots null) the workgroup adds to shard b % PB_CTR_SHARDS (one 128-B line per shard).
-#ifndef PB_COUNT
-#define PB_COUNT 1 // (A/B builds) 0: no counting at all (wrong counters; measures its cost)
-#endif
 // (pos: the record's index in the launch's slot array; pb_batch_kernel passes the part's own)
 __device__ __forceinline__ void pb_count_at(const pb_kargs &K, uint32_t b, uint32_t pos, uint64_t frames,
                                             uint64_t bytes)
 {
-    if (!PB_COUNT)
-        return;
     if (K.ctr_slots)
     {
         if (K.fixed_len)
@@ -446,9 +381,6 @@ extern "C" hipError_t pbk_launch_ctr_fold(const uint32_t *slots, uint64_t n, uin
 // checksum position at compile time; RANDOM selects the payload source.  The
 // frame body is straight-line code (no data-dependent control flow on d[]).
 
-#ifndef PB_RANGE_LDS
-#define PB_RANGE_LDS 0 // (A/B builds) pb_xpage_kernel reads the CIDR table from LDS
-#endif
 
 // keep bytes [lo, hi) of a dword (byte positions 0..3), branch-free
 __device__ __forceinline__ uint32_t pb_range_mask(int lo, int hi)
@@ -462,10 +394,8 @@ __device__ __forceinline__ uint32_t pb_range_mask(int lo, int hi)
 
 // One whole frame of <= 4*NDW bytes in VGPRs (iteration k = first_iter + fidx,
 // sequence.c:433-602): header fields, payload, L4 and IPv4 checksums.
-// rtab: (A/B builds, PB_RANGE_LDS) the CIDR table staged in LDS; null: K.ranges (global / L1)
 template <int NDW, int PROTO, bool RANDOM>
-__device__ __forceinline__ void pb_small_frame(const pb_kargs &K, uint64_t fidx, uint32_t (&d)[NDW],
-                                               const uint2 *rtab = nullptr)
+__device__ __forceinline__ void pb_small_frame(const pb_kargs &K, uint64_t fidx, uint32_t (&d)[NDW])
 {
     constexpr int HL = PROTO == 6 ? 54 : 42;
     constexpr int P0 = (HL - 2) / 4;                                 // payload byte 0 = byte 2 of dword P0
@@ -479,7 +409,7 @@ __device__ __forceinline__ void pb_small_frame(const pb_kargs &K, uint64_t fidx,
     uint32_t h[16];
     const uint32_t l4tot =
         pb_header(K, r0, plen, h,
-                  (rtab && (flags & PBK_RND_SADDR) && K.rng.d != 1) ? rtab[pb_mod(r0, K.rng)] : pb_range(K, r0));
+                  pb_range(K, r0));
 #pragma unroll
     for (int t = 0; t < NDW; ++t)
         d[t] = t < 16 ? h[t] : 0u;
@@ -646,16 +576,12 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
 // Linear form: workgroup b builds frames [WGT b, WGT b + WGT) and writes their
 // contiguous byte range (WGT = 256, or 128 / 64: smaller regions per workgroup).  Used when the output is not 4 KiB aligned (and under
 // PBGPU_KERNEL=linear for comparison).
-template <int NDW, int PROTO, bool RANDOM, int WGT, int AL = 0, bool NT = PB_SX_NT != 0> // AL: pb_small_put's alignment class
+template <int NDW, int PROTO, bool RANDOM, int WGT, int AL = 0> // AL: pb_small_put's alignment class
 __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
 {
-#if PB_SMALL_DYN
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[]; // pb_small_tile_bytes(WGT, flen)
-#else
-    __shared__ __attribute__((aligned(16))) uint32_t s_tile[WGT * NDW + 8];
-#endif
     const uint32_t tid = threadIdx.x;
-    const uint64_t f0 = (uint64_t)(PB_SMALL_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_rot) : blockIdx.x) * WGT;
+    const uint64_t f0 = (uint64_t)pb_xcd_region(blockIdx.x, gridDim.x) * WGT; // XCD-contiguous regions
     const uint64_t left = K.n_frames - f0;
     const uint32_t nfr = left < WGT ? (uint32_t)left : WGT;
     const uint32_t flen = K.fixed_len;
@@ -682,96 +608,79 @@ __global__ __launch_bounds__(WGT) void pb_small_kernel(pb_kargs K)
             for (int t = 0; t < 4; ++t)
                 v[t] &= pb_range_mask(0, (int)tile_bytes - (int)(16 * c + 4 * t));
         }
-        pb_st16_k<NT>(out + 16 * c, v);
+        pb_st16_nt(out + 16 * c, v);
     }
     if (tid == 0)
         pb_count(K, blockIdx.x, nfr, tile_bytes);
 }
 
-// XCD-owned form, for frame lengths that divide 4096 (64-B configs[1] frames,
-// 128-B frames).  The output stream (4 KiB aligned) is cut into 4 KiB pages of
-// fp = 4096 / flen whole frames; workgroup b, which the dispatcher deals to XCD
-// b % 8, owns pages ((b / 8) * np + i) * 8 + b % 8, i < np = 256 / fp, so every
-// XCD writes only the pages of one residue class mod 8.  Measured on MI355X
-// (tools/wbench.hip, profiles/r01/wbench): plain 16-B fills of 256-thread
-// workgroups with 4 stores per lane reach 6.0 TB/s over linear 16 KiB blocks and
-// 6.6 TB/s with this page ownership; 8 KiB pages, or 4 KiB pages off the 4 KiB
-// address grid, lose the gain.  Built here: 64-B UDP 0.35 -> 0.32 ms per 2 GiB.
-// Lengths that do not divide 4096 cut frames at page edges; building those
-// frames in both owners measured slower than the linear form (60-B TCP 0.37 vs
-// 0.345 ms, 98-B ICMP 0.70 vs 0.64), so they keep pb_small_kernel.
+// XCD-owned pages, one wave per page, for frame lengths that divide 4096 (64-B configs[1]
+// frames, 128-B frames).  The output stream (4 KiB aligned) is cut into 4 KiB pages of
+// fp = 4096 / flen whole frames.  Workgroup b, which the dispatcher deals to XCD b % 8, owns
+// NW * PPW pages, PPW = flen / 64 per wave (64 frames per wave, one per lane): wave w's page h is
+// c = (((b / 8) NW + w) PPW + h) 8 + b % 8, so every XCD writes only the pages of one residue
+// class mod 8, all eight inside one moving window.  A wave builds its frames into its own LDS
+// page, then stores the page as four 1-KiB store instructions: no workgroup barrier, each wave
+// starts storing as soon as its own frames are built.  Measured (profiles/r05/ab/xs*.jsonl,
+// 2^25 64-B frames, the same buffers): 0.3177 ms at 512 threads, 0.3223 at 256, vs 0.3325 for the
+// round-4 form (all four waves build, one barrier, every wave stores 1 KiB of each page); the
+// stores alone in the round-4 form took 0.3359 ms and the arithmetic alone 0.190, so the store
+// shape, not the arithmetic, set its time.  With the workgroups per CU capped by dynamic LDS
+// (K.lds_pad, pbgpu_load_sequence) the wave-local form runs at 0.297-0.303 ms on every buffer
+// (3 per CU), faster than the 4-KiB-per-workgroup plain fill beside it (0.309-0.312).
 
-// pages per workgroup of pb_xsmall_body's LDS tile
-template <int NDW, int WGT>
-constexpr uint32_t pb_xs_npg()
-{
-    return NDW == 16 ? (uint32_t)WGT / 64u : PB_XNP_MAX;
-}
-
-// workgroup b of nwg (b: the launch's blockIdx.x, or the part's own in pb_batch_kernel)
+// workgroup b of nwg (b: the launch's blockIdx.x, or the part's own in pb_batch_kernel); s_tile:
+// NW * PPW pages of 4 KiB
 template <int NDW, int PROTO, bool RANDOM, int WGT>
 __device__ __forceinline__ void pb_xsmall_body(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
 {
-    const uint32_t tid = threadIdx.x;
+    constexpr uint32_t NW = WGT / 64, PPW = NDW / 16; // waves; pages per wave (64 / 128-B frames)
+    constexpr uint32_t FPP = 64 / PPW;                // frames per page
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t flen = K.fixed_len;
-    const uint32_t np = K.xs_np;
     const uint64_t T = K.total_bytes;
-    uint32_t c0, cs;
-    if (b < K.xs_full)
+    const uint32_t m0 = ((b >> 3) * NW + w) * PPW; // the wave's first page's index within its XCD's class
+    uint32_t *const tile = s_tile + w * PPW * (PB_XPG / 4);
     {
-        if (PB_XS_XREMAP) // (A/B) XCD x takes the x-th contiguous eighth of the full groups' pages
-            c0 = pb_xcd_region(b, K.xs_full) * np, cs = 1;
-        else
-            c0 = (b >> 3) * (np * 8) + (b & 7u), cs = 8;
-    }
-    else
-        c0 = K.xs_full * np + (b - K.xs_full) * np, cs = 1;
-
-    // page i of the workgroup is frames [c_i * fp, (c_i + 1) * fp)
-    {
-        const uint32_t fps = K.xs_fp_shift; // fp = 1 << fps
-        const uint32_t i = tid >> fps, j = tid & ((1u << fps) - 1u);
-        const uint64_t f = ((uint64_t)(c0 + i * cs) << fps) + j;
-        if (f < K.n_frames)
+        const uint32_t h = lane / FPP, j = lane % FPP;
+        const uint32_t c = (m0 + h) * 8 + (b & 7u);
+        const uint64_t f = (uint64_t)c * FPP + j;
+        if (c < K.xs_nch && f < K.n_frames)
         {
             uint32_t d[NDW];
             pb_small_frame<NDW, PROTO, RANDOM>(K, f, d);
-            pb_small_put<NDW, true, 16>(s_tile, d, i * PB_XREG + 128 + j * flen, flen); // flen = 64 / 128 B
+            pb_small_put<NDW, true, 16>(tile, d, lane * flen, flen);
         }
     }
-    __syncthreads();
-
-    // page i -> HBM: 256 / WGT 16-B stores per lane per page (one at 256 threads; at 512, lane
-    // t stores chunk t % 256 of every other page)
-    constexpr uint32_t NPG = pb_xs_npg<NDW, WGT>();
-    constexpr uint32_t SPP = WGT >= 256 ? 1u : 256u / WGT, PPS = WGT >= 256 ? (uint32_t)WGT / 256u : 1u;
+    // the wave's LDS writes before its reads (a wave's LDS operations complete in order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (uint32_t u = 0; u < NPG * SPP / PPS; ++u)
+    for (uint32_t u = 0; u < 4 * PPW; ++u)
     {
-        const uint32_t i = WGT >= 256 ? u * PPS + tid / 256u : u / SPP;
-        const uint32_t ch = WGT >= 256 ? tid % 256u : (u % SPP) * WGT + tid;
-        const uint32_t c = c0 + i * cs;
+        const uint32_t h = u >> 2, ch = (u & 3u) * 64 + lane; // chunk ch of the wave's page h
+        const uint32_t c = (m0 + h) * 8 + (b & 7u);
         const uint64_t o = (uint64_t)c * PB_XPG + 16 * ch;
-        if (i < np && c < K.xs_nch && o < T)
+        if (c < K.xs_nch && o < T)
         {
-            const uint32_t sl = (i * PB_XREG + 128) / 16 + ch;
-            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[pb_swz(sl)];
+            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(tile)[pb_swz(h * 256 + ch)];
             if (o + 16 > T) // last chunk of the stream: zero the tail
             {
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
                     v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
             }
-            pb_st16_xs(K.out + o, v);
+            pb_st16_nt(K.out + o, v);
         }
     }
-    if (tid == 0)
+    if (threadIdx.x == 0)
     {
-        // the stored pages: whole frames (flen = 4096 >> xs_fp_shift divides every page)
+        // the workgroup's stored pages: whole frames (flen divides every page)
         uint64_t by = 0;
-        for (uint32_t i = 0; i < np; ++i)
+        for (uint32_t i = 0; i < NW * PPW; ++i)
         {
-            const uint32_t c = c0 + i * cs;
+            const uint32_t c = ((b >> 3) * NW * PPW + i) * 8 + (b & 7u);
             if (c < K.xs_nch)
                 by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
         }
@@ -779,11 +688,71 @@ __device__ __forceinline__ void pb_xsmall_body(const pb_kargs &K, uint32_t b, ui
     }
 }
 
-template <int NDW, int PROTO, bool RANDOM, int WGT = PB_WG> // 64-B frames: WGT / 64 pages per workgroup
+template <int NDW, int PROTO, bool RANDOM, int WGT = PB_WG>
 __global__ __launch_bounds__(WGT) void pb_xsmall_kernel(pb_kargs K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_tile[pb_xs_npg<NDW, WGT>() * PB_XREG / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[(WGT / 64) * (NDW / 16) * (PB_XPG / 4)];
     pb_xsmall_body<NDW, PROTO, RANDOM, WGT>(K, blockIdx.x, gridDim.x, s_tile);
+}
+
+// The round-4 64-B page body, kept for pb_batch_kernel's 64-B part: all WGT lanes build, one
+// barrier, then 256 lanes per page store it (the fused launch ran it 1% faster than the wave-local
+// body, 0.5335 vs 0.5386 ms per configs[4] step, profiles/r05/ab/mix*.jsonl: that launch runs at
+// the xpage parts' occupancy).  Workgroup b owns pages ((b / 8) np + i) 8 + b % 8, i < np =
+// WGT / 64 (the rest, fewer than 8 np, take the tail pages in order from xs_full).
+template <int WGT>
+__device__ __forceinline__ void pb_xsmall_wg_body(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
+{
+    constexpr uint32_t NPG = WGT / 64;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t np = K.xs_np;
+    const uint64_t T = K.total_bytes;
+    uint32_t c0, cs;
+    if (b < K.xs_full)
+        c0 = (b >> 3) * (np * 8) + (b & 7u), cs = 8;
+    else
+        c0 = K.xs_full * np + (b - K.xs_full) * np, cs = 1;
+    {
+        const uint32_t i = tid >> 6, j = tid & 63u;
+        const uint64_t f = ((uint64_t)(c0 + i * cs) << 6) + j;
+        if (f < K.n_frames)
+        {
+            uint32_t d[16];
+            pb_small_frame<16, 17, true>(K, f, d);
+            pb_small_put<16, true, 16>(s_tile, d, i * PB_XREG + 128 + j * 64, 64);
+        }
+    }
+    __syncthreads();
+    // page i -> HBM: lane t stores chunk t % 256 of pages t / 256, t / 256 + WGT / 256, ...
+#pragma unroll
+    for (uint32_t u = 0; u < NPG * 256 / WGT; ++u)
+    {
+        const uint32_t i = u * (WGT / 256) + tid / 256u, ch = tid % 256u;
+        const uint32_t c = c0 + i * cs;
+        const uint64_t o = (uint64_t)c * PB_XPG + 16 * ch;
+        if (i < np && c < K.xs_nch && o < T)
+        {
+            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[pb_swz((i * PB_XREG + 128) / 16 + ch)];
+            if (o + 16 > T)
+            {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
+            }
+            pb_st16_nt(K.out + o, v);
+        }
+    }
+    if (tid == 0)
+    {
+        uint64_t by = 0;
+        for (uint32_t i = 0; i < np; ++i)
+        {
+            const uint32_t c = c0 + i * cs;
+            if (c < K.xs_nch)
+                by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
+        }
+        pb_count_at(K, b, pb_xcd_region(b, nwg), 0, by);
+    }
 }
 
 // XCD-owned pages for frame lengths that are a multiple of 4 but do not divide
@@ -819,16 +788,6 @@ template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4>
 __device__ __forceinline__ void pb_xpage_body(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
 {
     const uint32_t tid = threadIdx.x;
-#if PB_RANGE_LDS
-    // (A/B) the CIDR table in LDS: one more barrier before the build
-    __shared__ uint2 s_rng[64];
-    if (tid < K.rng.d && tid < 64u && (K.flags & PBK_RND_SADDR))
-        s_rng[tid] = K.ranges[tid];
-    __syncthreads();
-    const uint2 *const rtab = s_rng;
-#else
-    const uint2 *const rtab = nullptr;
-#endif
     const uint32_t flen = K.fixed_len;
     const uint32_t np = K.xs_np, fpp = K.xp_fpp;
     const uint64_t T = K.total_bytes;
@@ -867,7 +826,7 @@ __device__ __forceinline__ void pb_xpage_body(const pb_kargs &K, uint32_t b, uin
         if (off >= (int)PB_XPG || f >= K.n_frames)
             continue;
         uint32_t d[NDW];
-        pb_small_frame<NDW, PROTO, RANDOM>(K, f, d, rtab);
+        pb_small_frame<NDW, PROTO, RANDOM>(K, f, d);
         if (A4)
         {
             // 4-B aligned: dword pairs (ds_write2_b32 / ds_write_b64), a last single dword
@@ -901,7 +860,7 @@ __device__ __forceinline__ void pb_xpage_body(const pb_kargs &K, uint32_t b, uin
                 for (int t = 0; t < 4; ++t)
                     v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
             }
-            pb_st16_sx(K.out + o, v);
+            pb_st16_nt(K.out + o, v);
         }
     }
     if (tid == 0)
@@ -919,8 +878,11 @@ __device__ __forceinline__ void pb_xpage_body(const pb_kargs &K, uint32_t b, uin
     }
 }
 
+// (an SGPR budget of 80, as pb_batch_kernel: 8 waves per SIMD instead of 6-7; 60-B TCP SYN
+// 0.282-0.291 vs 0.302-0.308 ms, 98-B ICMP 0.457-0.471 vs 0.478-0.488 on four buffers,
+// profiles/r05/ab/xp.jsonl)
 template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4 = true> // A4: flen % 4 == 0 (else 2 mod 4)
-__global__ __launch_bounds__(WGT) void pb_xpage_kernel(pb_kargs K)
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pb_xpage_kernel(pb_kargs K)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[]; // K.xs_np page regions
     pb_xpage_body<NDW, PROTO, RANDOM, WGT, A4>(K, blockIdx.x, gridDim.x, s_tile);
@@ -949,15 +911,17 @@ __device__ __forceinline__ void pb_batch_part(const pb_kargs &K, uint32_t b, uin
     if (b >= nwg) // the padding before the next part's first workgroup
         return;
     if constexpr (KIND == 1)
-        pb_xsmall_body<16, 17, true, WGT>(K, b, nwg, s_tile);
+        pb_xsmall_wg_body<WGT>(K, b, nwg, s_tile);
     else if constexpr (KIND == 2)
         pb_xpage_body<16, 6, true, WGT, true>(K, b, nwg, s_tile);
     else
         pb_xpage_body<32, 1, false, WGT, false>(K, b, nwg, s_tile);
 }
 
+// (an SGPR budget of 80: the compiler's 106 admit 6 waves per SIMD, 3 workgroups of 512 threads
+// per CU, 80 admit 8: 0.5335 vs 0.5484 ms per configs[4] step, profiles/r05/ab/mix*.jsonl)
 template <int WGT, int KA, int KB, int KC>
-__global__ __launch_bounds__(WGT) void pb_batch_kernel(pb_batch_args A)
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pb_batch_kernel(pb_batch_args A)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];
     const uint32_t b = blockIdx.x;
@@ -1293,28 +1257,6 @@ __global__ __launch_bounds__(PB_WG) void pb_gpf_kernel(pb_kargs K)
 //      byte-exact over the stage.
 //   S  the window streamed to HBM as one contiguous run of 16-B stores; only the
 //      two chunks shared with the neighbouring windows are byte-masked.
-#ifndef PB_TIMING
-#define PB_TIMING 0
-#endif
-// diagnostic builds (-DPB_TIMING=1): per-workgroup stamps, slots 0 and 6 in the
-// 100 MHz real-time clock, slots 1..4 in shader cycles (summed over windows)
-#define PB_STAMP(i)                                                                                   \
-    do                                                                                                \
-    {                                                                                                 \
-        if (PB_TIMING && tid == 0 && K.dbg)                                                           \
-            K.dbg[(uint64_t)blockIdx.x * 8 + (i)] =                                                   \
-                ((i) == 0 || (i) == 6) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#define PB_LAP(i, t)                                                                                  \
-    do                                                                                                \
-    {                                                                                                 \
-        if (PB_TIMING && tid == 0 && K.dbg)                                                           \
-        {                                                                                             \
-            const unsigned long long now = __builtin_amdgcn_s_memtime();                              \
-            K.dbg[(uint64_t)blockIdx.x * 8 + (i)] += now - (t);                                       \
-            (t) = now;                                                                                \
-        }                                                                                             \
-    } while (0)
 
 template <int G, int RMODE, int WGT>
 __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
@@ -1342,10 +1284,6 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
     const uint32_t nfr = left < WF ? (uint32_t)left : WF;
     const uint64_t W0 = K.fixed_len ? f0 * K.fixed_len : K.offsets[f0];
     const uint64_t wbase = W0 & ~15ull;
-    unsigned long long tlap = 0;
-    PB_STAMP(0);
-    if (PB_TIMING && tid == 0)
-        tlap = __builtin_amdgcn_s_memtime();
 
     // ---------------- A: one lane per frame ----------------
     // the table loads are issued first; their latency hides behind the seed arithmetic
@@ -1449,7 +1387,6 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
     }
     __syncthreads();
     const uint32_t nwin = s_r[nfr - 1] / W + 1;
-    PB_LAP(1, tlap);
 
     constexpr uint32_t NGW = WGT / G; // frames in flight per workgroup
     const uint32_t grp = tid / G, lg = tid % G;
@@ -1514,7 +1451,6 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
             }
         }
         __syncthreads();
-        PB_LAP(2, tlap);
 
         // ---------------- C: headers -> stage, one lane per (frame, dword) ----------------
         for (uint32_t t = tid; t < (se - sb) * 16; t += WGT)
@@ -1540,7 +1476,6 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
             }
         }
         __syncthreads();
-        PB_LAP(3, tlap);
 
         // ---------------- S: stage -> HBM, contiguous 16-B stores ----------------
         // whole chunks [c0, c1) two per lane per step (both LDS reads in flight
@@ -1570,9 +1505,7 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
             pb_store_chunk(gout + 16 * c1, v[0], v[1], v[2], v[3], (int)(16 * c1) - (int)lo_b, (int)(hi_b - lo_b));
         }
         __syncthreads(); // the next window reuses the stage
-        PB_LAP(4, tlap);
     }
-    PB_STAMP(6);
     if (tid == 0 && nfr) // the windows stored the workgroup's frames' bytes, each once
         pb_count(K, blockIdx.x, nfr, s_r[nfr - 1] + s_len[nfr - 1] - s_r[0]);
 }
@@ -1600,7 +1533,7 @@ __global__ __launch_bounds__(WGT) void pb_stage_kernel(pb_kargs K)
 //    pseudo-header word sum minus the generated header bytes of the first payload
 //    chunk (overwritten by the header), so the group reduction is the whole sum.
 //  * Two stage buffers: window w + 1 is generated while window w's stores drain.
-template <int G, bool L4, bool NT = PB_FS_NT != 0> // NT: non-temporal frame stores
+template <int G, bool L4>
 __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
 {
     constexpr uint32_t NGW = PB_WG / G; // frames per window
@@ -1614,11 +1547,7 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
     const uint32_t tid = threadIdx.x;
     const uint32_t flags = K.flags;
     const uint32_t flen = K.fixed_len, hl = K.hl;
-    unsigned long long tt = 0; // PB_TIMING builds: phase stamps (slot 1 A, 2 B, 4 S)
-    PB_STAMP(0);
-    if (PB_TIMING)
-        tt = __builtin_amdgcn_s_memtime();
-    const uint64_t f0 = (uint64_t)(PB_FST_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_rot) : blockIdx.x) * WF;
+    const uint64_t f0 = (uint64_t)pb_xcd_region(blockIdx.x, gridDim.x) * WF;
     const uint64_t left = K.n_frames - f0;
     const uint32_t nfr = left < WF ? (uint32_t)left : WF;
     const uint64_t W0 = f0 * flen; // 16-B aligned
@@ -1640,7 +1569,7 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
 
     // ---------------- A: one lane per frame ----------------
     const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
-    if (tid < nfr && !(K.fst_dbg & 8u))
+    if (tid < nfr)
     {
         const uint64_t f = f0 + tid;
         const uint32_t hs0 = (((tid % NGW) * flen) & 15u) + hl;
@@ -1680,7 +1609,6 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
         }
     }
     __syncthreads();
-    PB_LAP(1, tt);
 
     const uint32_t nwin = (nfr + NGW - 1) / NGW;
     const uint32_t hw = hl >> 2; // header dwords written whole; hl % 4 == 2: one more half dword
@@ -1693,7 +1621,7 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
         const bool live = grp < nfw;
         // ---------------- B: payload chunks, then the group's header ----------------
         uint32_t acc = 0;
-        if (live && cnt && !(K.fst_dbg & 1u))
+        if (live && cnt)
         {
             if (L4 && lg == 0)
                 acc = s_a0[fr];
@@ -1730,7 +1658,7 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
         }
         if (L4)
             acc = pb_group_sum<G>(acc);
-        if (live && lg <= hw && !(K.fst_dbg & 1u))
+        if (live && lg <= hw)
         {
             uint32_t v = s_img[fr * 16 + lg];
             if (L4)
@@ -1746,7 +1674,6 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
                 *reinterpret_cast<uint16_t *>(hp) = (uint16_t)v;
         }
         __syncthreads();
-        PB_LAP(2, tt);
 
         // ---------------- S: the window to HBM, contiguous 16-B stores ----------------
         // window bytes [0, R1); a last chunk that is not whole (the launch's last,
@@ -1760,17 +1687,17 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
         const uint64_t gb = W0 + (uint64_t)w * NGW * flen;
         uint8_t *const gout = K.out + gb;
         const pb_u32x4 *const st16 = reinterpret_cast<const pb_u32x4 *>(stg);
-        uint32_t c = (K.fst_dbg & 2u) ? c1 : ((tid - (uint32_t)(gb >> 4)) & (PB_WG - 1u));
+        uint32_t c = (tid - (uint32_t)(gb >> 4)) & (PB_WG - 1u);
         for (; c + 3 * PB_WG < c1; c += 4 * PB_WG)
         {
             const pb_u32x4 v0 = st16[c], v1 = st16[c + PB_WG], v2 = st16[c + 2 * PB_WG], v3 = st16[c + 3 * PB_WG];
-            pb_st16_k<NT>(gout + 16 * c, v0);
-            pb_st16_k<NT>(gout + 16 * (c + PB_WG), v1);
-            pb_st16_k<NT>(gout + 16 * (c + 2 * PB_WG), v2);
-            pb_st16_k<NT>(gout + 16 * (c + 3 * PB_WG), v3);
+            pb_st16(gout + 16 * c, v0);
+            pb_st16(gout + 16 * (c + PB_WG), v1);
+            pb_st16(gout + 16 * (c + 2 * PB_WG), v2);
+            pb_st16(gout + 16 * (c + 3 * PB_WG), v3);
         }
         for (; c < c1; c += PB_WG)
-            pb_st16_k<NT>(gout + 16 * c, st16[c]);
+            pb_st16(gout + 16 * c, st16[c]);
         if (tid == PB_WG - 1 && (R1 & 15u))
         {
             const uint32_t *sw = reinterpret_cast<const uint32_t *>(stg) + 4 * c1;
@@ -1782,11 +1709,9 @@ __global__ __launch_bounds__(PB_WG) void pb_fstage_kernel(pb_kargs K)
             __syncthreads(); // the next window reuses the stage
         else
             sb = sb ? 0u : SB;
-        PB_LAP(4, tt);
     }
-    PB_STAMP(6);
-    if (tid == 0) // (PBGPU_FST_DBG bit 1 skips the stores: nothing stored, nothing counted)
-        pb_count(K, blockIdx.x, nfr, (K.fst_dbg & 2u) ? 0ull : (uint64_t)nfr * flen);
+    if (tid == 0)
+        pb_count(K, blockIdx.x, nfr, (uint64_t)nfr * flen);
 }
 
 // ---------------- any length, every payload random: pb_vstage_kernel ----------------
@@ -1832,13 +1757,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     uint32_t *const s_ord = s_win + CAP + 2; // frames of each window, longest first
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t bxr = PB_VST_XREMAP ? pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_rot) : blockIdx.x; // region
+    const uint32_t bxr = pb_xcd_region(blockIdx.x, gridDim.x); // region
     const uint32_t flags = K.flags;
     const uint32_t hl = K.hl;
-    unsigned long long tt = 0; // PB_TIMING builds: phase stamps (slot 1 A, 3 windows + order, 2 B, 4 S)
-    PB_STAMP(0);
-    if (PB_TIMING)
-        tt = __builtin_amdgcn_s_memtime();
     // Workgroup b owns frames [f0, f0 + nown) and stores exactly the output bytes
     // [lo, hi): lo = the 128-B line holding its first frame's start (0 for b = 0), hi =
     // the next workgroup's lo.  No line is written by two workgroups (two XCDs): an
@@ -1851,8 +1772,8 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     const uint64_t left = K.n_frames - f0;
     const uint32_t nown = left < WF ? (uint32_t)left : WF;
     const uint64_t fe = f0 + nown;
-    // (PBGPU_FST_DBG bit 6, A/B only: the round-1 edges at the frame starts, lines split)
-    const uint64_t emask = (K.fst_dbg & 64u) ? ~0ull : ~127ull;
+    // (PBGPU_VST_SHAPE bit 6: the round-1 edges at the frame starts, lines split)
+    const uint64_t emask = (K.vst_shape & 64u) ? ~0ull : ~127ull;
 
     // ---------------- A: one lane per slot; the stage starts zero ----------------
     // Slot j holds frame f0 - PB_VST_GHOSTS + j: the possible ghosts, then the own
@@ -1991,7 +1912,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             s_hs[tix] = hsf;
     }
     __syncthreads();
-    PB_LAP(1, tt);
     const uint32_t my_r = tid < nfr ? s_r[tid] : 0u;
     // window starts: frame t opens windows (r_{t-1} / W, r_t / W]  (W >= the longest frame)
     if (tid < nfr)
@@ -2015,7 +1935,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         const uint32_t w = my_r / W;
         const uint32_t b = s_win[w], e = s_win[w + 1];
         uint32_t rank = tid - b;
-        if (e - b <= 64 && !(K.fst_dbg & 256u))
+        if (e - b <= 64 && !(K.vst_shape & 256u))
         {
             const uint32_t len = s_len[tid];
             rank = 0;
@@ -2028,7 +1948,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         s_ord[b + rank] = tid;
     }
     __syncthreads();
-    PB_LAP(3, tt);
 
     for (uint32_t w = 0; w < nwin; ++w)
     {
@@ -2044,13 +1963,13 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         bool any32 = false; // (workgroup-uniform) a 32-lane group exists in this window
         // the layout's counts assume 256 lanes: 32 y + 16 x == 256 for 9-16 frames, 32 F <= 256 for F <= 8
         static_assert(PB_WG == 256, "pb_vstage_kernel's 32/16/8-lane window layout is for 256-thread workgroups");
-        if (G == 8 && !(K.fst_dbg & 16u))
+        if (G == 8 && !(K.vst_shape & 16u))
         {
             const uint32_t F = se - sb;
             uint32_t y = 0, x = 0;
             if (F <= 16u)
             {
-                y = K.fst_dbg & 32u ? 0u : (F <= 8u ? F : 16u - F);
+                y = K.vst_shape & 32u ? 0u : (F <= 8u ? F : 16u - F);
                 x = F - y;
             }
             else if (F <= 32u)
@@ -2066,7 +1985,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         const uint2 MG = s_l48[g];
 
         // ---------------- B: g lanes per frame, payload chunks, then the header ----------------
-        for (uint32_t k = sb + grp0; k < (K.fst_dbg & 1u ? sb : se); k += NGW)
+        for (uint32_t k = sb + grp0; k < se; k += NGW)
         {
             const uint32_t fr = s_ord[k];
             const uint32_t r = s_r[fr] - sbase;
@@ -2167,7 +2086,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         __syncthreads();
         const uint32_t mh = (hl + 30u) >> 4;
         const uint32_t mhinv = (65536u + mh - 1u) / mh;
-        const uint32_t nhl = (K.fst_dbg & 1u) ? 0u : (se - sb) * mh;
+        const uint32_t nhl = (se - sb) * mh;
         for (uint32_t i = tid; i < nhl; i += PB_WG)
         {
             const uint32_t ti = __umul24(i, mhinv) >> 16; // i / mh (exact for i < 2^12, mh <= 8)
@@ -2219,7 +2138,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
             }
         }
         __syncthreads();
-        PB_LAP(2, tt);
 
         // ---------------- S: stage -> HBM, contiguous 16-B stores, then zero ----------------
         // the window's bytes [R0, R1) clipped to the workgroup's [lo, hi): whole chunks
@@ -2228,7 +2146,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         // A chunk shared with the next window of this workgroup is not stored here: its value
         // is carried into the next window's stage chunk 0 (the same 16 B of output) and stored
         // whole with that window (masked byte stores by one lane per window edge made S ~25%
-        // of a workgroup's life).  Only workgroup edges (128-B aligned unless PBGPU_FST_DBG bit 6)
+        // of a workgroup's life).  Only workgroup edges (128-B aligned unless PBGPU_VST_SHAPE bit 6)
         // and the launch's end keep masked stores.
         const uint32_t R0c = R0 > lo_rel ? R0 : lo_rel, R1c = R1 < hi_rel ? R1 : hi_rel;
         uint32_t cf0 = 0, cf1 = 0;
@@ -2260,8 +2178,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
                                (int)(hi_b - lo_b));
             }
         }
-        if (K.fst_dbg & 2u)
-            cf1 = cf0;
         // (one chunk per step: four LDS reads in flight, then four stores, measured 1.7%
         // slower on configs[2])
         for (uint32_t c = cf0 + ((tid - cf0) & (PB_WG - 1u)); c < cf1; c += PB_WG)
@@ -2271,11 +2187,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
         // window's payload barrier), never a payload chunk, so this plain write is its first
         if (cout && tid == (chc & (PB_WG - 1u)))
             stage[0] = cv;
-        PB_LAP(4, tt);
     }
-    PB_STAMP(6);
-    if (tid == 0) // the workgroup stores exactly [lo, hi) (PBGPU_FST_DBG bit 1: the stores are skipped)
-        pb_count(K, bxr, nown, (K.fst_dbg & 2u) ? 0ull : hi_abs - lo_abs);
+    if (tid == 0) // the workgroup stores exactly [lo, hi)
+        pb_count(K, bxr, nown, hi_abs - lo_abs);
 }
 
 // ---------------- packed variable lengths, stores straight from registers: pb_vline_kernel ----------------
@@ -2337,12 +2251,6 @@ constexpr uint32_t pb_inv24(uint32_t a)
 constexpr uint32_t PB_A3I = pb_inv24(PB_A3 & PB_M24);
 constexpr uint32_t PB_C3I = (0u - PB_A3I * (PB_C3 & PB_M24)) & PB_M24;
 static_assert(((PB_A3I * (PB_A3 & PB_M24)) & PB_M24) == 1u, "M^-1");
-#ifndef PB_ORB_LOG12
-#define PB_ORB_LOG12 1 // pb_orbit_sum: the discrete log's top 12 bits in closed form (0: 24 steps)
-#endif
-#ifndef PB_ORB_BIDIR
-#define PB_ORB_BIDIR 1 // pb_orbit_sum walks to the nearer prefix-sum sample (<= 16 steps; 0: the next, <= 31)
-#endif
 
 // Little-endian 16-bit word sum (mod 0xFFFF, in [1, 0xFFFF]) of the n >= 3 payload bytes drawn
 // from the LCG state st0 entering the payload (sequence.c:552-555), payload at an even L4 offset:
@@ -2352,7 +2260,6 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
 {
     const uint32_t yp = (PB_A3 * st0 + PB_C3) & PB_M24; // the state of payload byte 0
     uint32_t cur = 0, p = 0;
-#if PB_ORB_LOG12
     // bits 0-11 one at a time; bits 12-23 in closed form: with N = M^4096 = (A, C), A = 1 + 2^14 u,
     // C = 2^12 v (v odd), N^j(x) = x + j ((A - 1) x + C) mod 2^24 (the dropped terms carry 2^26), so
     // j = ((yp - cur) >> 12) / (((A - 1) >> 12) yp + v) mod 2^12 (the divisor is odd)
@@ -2375,32 +2282,18 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
         const uint32_t j = __umul24(((yp - cur) >> 12) & 0xFFFu, x) & 0xFFFu;
         p |= j << 12;
     }
-#else
-#pragma unroll
-    for (int i = 0; i < 24; ++i)
-    {
-        const uint32_t bit = 1u << i;
-        const uint32_t nx = __umul24(cur, pb_orb_a(i)) + pb_orb_c(i);
-        const bool take = ((cur ^ yp) & bit) != 0;
-        cur = take ? nx : cur;
-        p |= take ? bit : 0u;
-    }
-#endif
     const uint2 jq = K.jump[n - 1 + PB_JNEG]; // L^(3n): the state one past the payload
     const uint32_t yq = jq.x * yp + jq.y;
     uint32_t q = p + n, wrap = 0;
     if (q >= (1u << 24)) // the run wraps the orbit (2^24 is even: parities keep)
         q -= 1u << 24, wrap = K.orbit_tot;
-#if PB_ORB_BIDIR
     // prefix sums at p and q from the nearer sampled position (floor or ceil, <= 16 steps): walk the
     // bytes in between with M (forward, subtract) or M^-1 (backward, add); a[t & 1] collects the
     // walked bytes of one parity, the first walked position having parity par
     constexpr uint32_t SM = (1u << PB_ORB_SH) - 1u, HALF = (SM + 1u) >> 1;
     const bool fp = (p & SM) > HALF, fq = (q & SM) > HALF; // forward to the next sample
-    // (PBGPU_FST_DBG bit 6, diagnostics: the table entries replaced by their indices, no loads)
     const uint32_t ip = (p >> PB_ORB_SH) + (fp ? 1u : 0u), iq = (q >> PB_ORB_SH) + (fq ? 1u : 0u);
-    const bool noload = (K.fst_dbg & 64u) != 0;
-    const uint32_t tp = noload ? ip : K.orbit[ip], tq = noload ? iq : K.orbit[iq];
+    const uint32_t tp = K.orbit[ip], tq = K.orbit[iq];
     const uint32_t dp = fp ? SM + 1u - (p & SM) : (p & SM), dq = fq ? SM + 1u - (q & SM) : (q & SM);
     const uint32_t ap_ = fp ? PB_A3 & PB_M24 : PB_A3I, cp_ = fp ? PB_C3 & PB_M24 : PB_C3I;
     const uint32_t aq_ = fq ? PB_A3 & PB_M24 : PB_A3I, cq_ = fq ? PB_C3 & PB_M24 : PB_C3I;
@@ -2425,42 +2318,12 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     const uint32_t POq = fq ? (tq >> 16) + 0xFFFFu - sOq : (tq >> 16) + sOq;
     const uint32_t de = PEq + wrap + 2u * 0xFFFFu - PEp;
     const uint32_t dO = POq + wrap + 2u * 0xFFFFu - POp;
-#else
-    constexpr uint32_t SM = (1u << PB_ORB_SH) - 1u;
-    const uint32_t tp = K.orbit[(p + SM) >> PB_ORB_SH], tq = K.orbit[(q + SM) >> PB_ORB_SH];
-    // prefix sums at p and q from the next sampled position, minus the bytes in between (walked
-    // with the LCG; a[t & 1] collects the bytes at positions p + t of one parity)
-    uint32_t ap[2] = {0u, 0u}, aq[2] = {0u, 0u};
-    uint32_t y = yp, z = yq;
-    const uint32_t cp = (SM + 1u - (p & SM)) & SM, cq = (SM + 1u - (q & SM)) & SM;
-#pragma unroll
-    for (uint32_t t = 0; t < SM; ++t)
-    {
-        ap[t & 1u] += t < cp ? (y >> 16) & 0xFFu : 0u;
-        aq[t & 1u] += t < cq ? (z >> 16) & 0xFFu : 0u;
-        y = __umul24(y, PB_A3) + PB_C3;
-        z = __umul24(z, PB_A3) + PB_C3;
-    }
-    const uint32_t e_p = ap[p & 1u], o_p = ap[(p & 1u) ^ 1u], e_q = aq[q & 1u], o_q = aq[(q & 1u) ^ 1u];
-    // PE(q) - PE(p), PO(q) - PO(p), kept positive with multiples of 0xFFFF
-    const uint32_t de = (tq & 0xFFFFu) + wrap + e_p + 2u * 0xFFFFu - e_q - (tp & 0xFFFFu);
-    const uint32_t dO = (tq >> 16) + wrap + o_p + 2u * 0xFFFFu - o_q - (tp >> 16);
-#endif
     // payload byte j sits at orbit position p + j: even j is a word's low byte
     const uint32_t s = (p & 1u) ? dO + (de << 8) : de + (dO << 8);
     return pb_fold(s);
 }
 
-#ifndef PB_VL_SPLIT
-#define PB_VL_SPLIT 1
-#endif
-#ifndef PB_VL_LATE
-#define PB_VL_LATE 1 // pb_vline_kernel: the L4 checksum is folded into the header image after the scan
-#endif
-#ifndef PB_VL_IMGW
-#define PB_VL_IMGW 1 // prologue: header images as NHW dword writes, line map as plain writes + the last line
-#endif
-template <int HL, bool L4, bool NT = PB_VL_NT != 0> // NT: non-temporal frame stores
+template <int HL, bool L4>
 __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
 {
     constexpr uint32_t GH = PB_VST_GHOSTS;
@@ -2478,7 +2341,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     uint16_t *const s_map = reinterpret_cast<uint16_t *>(s_l48 + K.vl_nl48);
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t bxr = pb_xcd_region(blockIdx.x, gridDim.x, K.xcd_rot); // XCD-contiguous regions
+    const uint32_t bxr = pb_xcd_region(blockIdx.x, gridDim.x); // XCD-contiguous regions
     const uint32_t flags = K.flags;
     const uint64_t f0 = (uint64_t)bxr * WF;
     const uint64_t left = K.n_frames - f0;
@@ -2486,36 +2349,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     const uint64_t fe = f0 + nown;
 
     const uint32_t lane = tid & 63u, wv = tid >> 6;
-    if (K.fst_dbg & 16u)
-    {
-        // (PBGPU_FST_DBG bit 4, diagnostics: the stream's stores alone over the launch's own
-        // regions, no prologue — the store shape's time)
-        uint64_t part = 0;
-        for (uint32_t t = tid; t < (bxr & 255u); t += PB_WG)
-            part += K.vblk_sum[(bxr & ~255u) + t];
-#pragma unroll
-        for (uint32_t dd = 32; dd > 0; dd >>= 1)
-            part += __shfl_xor(part, dd, 64);
-        if (lane == 0u)
-            reinterpret_cast<uint64_t *>(s_dyn)[wv] = part;
-        __syncthreads();
-        uint64_t S = K.vblk_l2[bxr >> 8];
-#pragma unroll
-        for (uint32_t w = 0; w < PB_WG / 64; ++w)
-            S += reinterpret_cast<uint64_t *>(s_dyn)[w];
-        const uint64_t lo = bxr ? (S & ~127ull) : 0ull;
-        const uint64_t hi = bxr + 1u < gridDim.x ? ((S + K.vblk_sum[bxr]) & ~127ull) : lo;
-        const uint32_t R = (uint32_t)(hi - lo);
-        for (uint32_t s = 0; s < (R + PB_VL_STEP - 1u) / PB_VL_STEP; ++s)
-#pragma unroll
-            for (uint32_t i = 0; i < 4; ++i)
-            {
-                const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
-                if (c0 < R)
-                    pb_st16_k<NT>(K.out + lo + c0, pb_u32x4{c0, s, i, (uint32_t)lo});
-            }
-        return;
-    }
 
     // ---------------- prologue: one lane per frame slot ----------------
     const int64_t fb = (int64_t)f0 - (int64_t)GH;
@@ -2536,8 +2369,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
 #pragma unroll
     for (int w = 0; w < 16; ++w)
         d[w] = 0u;
-    uint32_t csum_v = 0; // PB_VL_LATE: the L4 checksum field, ORed into d[] after the scan
-    constexpr bool vl_late = PB_VL_LATE != 0;
+    uint32_t csum_v = 0; // the L4 checksum field, ORed into d[] after the scan
     if (valid)
     {
         uint64_t k;
@@ -2557,16 +2389,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
                           pb_halves(d[13]);
             if (flags & PBK_PSEUDO)
                 hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
-            // (PBGPU_FST_DBG bit 5, diagnostics: no payload sum, the orbit-table reads skipped)
-            const uint32_t ps = (K.fst_dbg & 32u) ? 0u : pb_orbit_sum(K, P.st0, P.plen);
+            const uint32_t ps = pb_orbit_sum(K, P.st0, P.plen);
             const uint32_t c = (~pb_fold(pb_fold(hs) + ps)) & 0xFFFFu;
             csum_v = K.csum_hi ? (c << 16) : c;
-            if (!vl_late)
-            {
-#pragma unroll
-                for (uint32_t w = 0; w < 16; ++w)
-                    d[w] |= w == K.csum_dw ? csum_v : 0u;
-            }
         }
     }
     // frame starts: exclusive scan of the slot lengths (in-wave shuffles, wave totals via LDS)
@@ -2625,14 +2450,11 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     const int32_t tix = (int32_t)tid - (int32_t)(GH - ng);
     if (valid && tix >= 0)
     {
-        if (vl_late)
-        {
-            // the checksum only now: the orbit-table loads behind it (issued in the frame's
-            // field computation) complete under the scan and the barrier instead of before them
+        // the checksum only now: the orbit-table loads behind it (issued in the frame's field
+        // computation) complete under the scan and the barrier instead of before them
 #pragma unroll
-            for (uint32_t w = 0; w < 16; ++w)
-                d[w] |= w == K.csum_dw ? csum_v : 0u;
-        }
+        for (uint32_t w = 0; w < 16; ++w)
+            d[w] |= w == K.csum_dw ? csum_v : 0u;
         const uint32_t r = (uint32_t)(start - wbase);
         const uint32_t s0 = r & 15u;
         const uint2 jt = s_jt[s0];
@@ -2647,7 +2469,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             const uint32_t lo = u > 0 ? d[u - 1] : 0u, hi = u < 16 ? d[u] : 0u;
             v[u] = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
         }
-#if PB_VL_IMGW
         // only the header bytes [s0, s0 + HL) of the image chunks are ever read (bytes before s0
         // belong to the previous frame's chunk and take its payload, bytes after the header this
         // frame's payload): NHW dwords from dword q, inside the frame's own NSP chunks
@@ -2657,25 +2478,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
 #pragma unroll
         for (uint32_t u = 0; u < NHW; ++u)
             img32[u] = v[u];
-#else
-        pb_u32x4 *const img = s_img + (uint32_t)tix * NSP;
-#pragma unroll
-        for (uint32_t j = 0; j < NSP; ++j)
-        {
-            uint32_t o[4];
-#pragma unroll
-            for (uint32_t t = 0; t < 4; ++t)
-            {
-                const int u = (int)(4 * j + t);
-                const uint32_t a0 = u < 17 ? v[u] : 0u;
-                const uint32_t a1 = u >= 1 && u - 1 < 17 ? v[u - 1] : 0u;
-                const uint32_t a2 = u >= 2 && u - 2 < 17 ? v[u - 2] : 0u;
-                const uint32_t a3 = u >= 3 && u - 3 < 17 ? v[u - 3] : 0u;
-                o[t] = q == 0 ? a0 : (q == 1 ? a1 : (q == 2 ? a2 : a3));
-            }
-            img[j] = pb_u32x4{o[0], o[1], o[2], o[3]};
-        }
-#endif
     }
     __syncthreads();
 
@@ -2694,23 +2496,17 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         // 8: none), kept as 8 - c in bits 0-2 and 4-6: chunk k of the line lies in frame
         // tix + (k >= c1) + (k >= c2), and k >= c <=> k + (8 - c) carries into bit 3 / 7
         const uint32_t b2 = (uint32_t)tix + 1u < nfr ? s_rec[tix + 1][2] - lo_rel : 0xFFFFFFFFu;
-#if PB_VL_IMGW
         // only the frame's last line can hold the next frame starts (o1, o2 >= 128 before it)
         for (uint32_t L = la; L + 1u < lb; ++L)
             s_map[L] = (uint16_t)((uint32_t)tix << 8);
         if (la < lb)
         {
             const uint32_t L = lb - 1u;
-#else
-        for (uint32_t L = la; L < lb; ++L)
-        {
-#endif
             const uint32_t o1 = b - (L << 7), o2 = b2 - (L << 7);
             const uint32_t c1 = o1 < 128u ? (o1 + 15u) >> 4 : 8u, c2 = o2 < 128u ? (o2 + 15u) >> 4 : 8u;
             s_map[L] = (uint16_t)(((uint32_t)tix << 8) | (8u - c1) | ((8u - c2) << 4));
         }
     }
-#if PB_VL_MT
     // chunk byte masks, indexed by plo + phi: a chunk holds a payload start (plo > 0, phi = 16) or
     // a payload end (plo = 0, phi < 16) or neither (payloads of >= 32 B), so s_m16[j] keeps bytes
     // < j for j <= 16 and bytes >= j - 16 above
@@ -2720,11 +2516,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         s_m16[tid] = pb_u32x4{pb_range_mask(lo, hi), pb_range_mask(lo - 4, hi - 4), pb_range_mask(lo - 8, hi - 8),
                               pb_range_mask(lo - 12, hi - 12)};
     }
-#else
-    if (tid <= 16u) // chunk byte masks: s_m16[k] keeps bytes >= k
-        s_m16[tid] = pb_u32x4{pb_range_mask((int)tid, 4), pb_range_mask((int)tid - 4, 4), pb_range_mask((int)tid - 8, 4),
-                              pb_range_mask((int)tid - 12, 4)};
-#endif
     if (tid == 64u) // the header chunk after the last record's: no frame starts there
         s_img[nfr * NSP] = pb_u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
@@ -2737,19 +2528,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     // next frame's first chunk, bytes >= phi; for a chunk with neither both masks are empty).
     // One straight-line path per chunk, and every 128-B line leaves in one store instruction.
     uint8_t *const gout = K.out + wbase + lo_rel;
-    const bool store = !(K.fst_dbg & 2u);
-    // (PBGPU_FST_DBG diagnostics: bit 0 the prologue alone, no stream; bit 2 the stream's stores
-    // alone, a constant per chunk)
-    const uint32_t nsteps = (K.fst_dbg & 5u) ? 0u : (R + PB_VL_STEP - 1u) / PB_VL_STEP;
-    if (K.fst_dbg & 4u)
-        for (uint32_t s = 0; s < (R + PB_VL_STEP - 1u) / PB_VL_STEP; ++s)
-#pragma unroll
-            for (uint32_t i = 0; i < 4; ++i)
-            {
-                const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
-                if (c0 < R)
-                    pb_st16_k<NT>(gout + c0, pb_u32x4{c0, s, i, lo_rel});
-            }
+    const uint32_t nsteps = (R + PB_VL_STEP - 1u) / PB_VL_STEP;
     const uint32_t k = lane & 7u, kk = k | (k << 4), ck = (lo_rel >> 4) + k;
     const uint32_t lmax = nlines ? nlines - 1u : 0u;
     // chunk i of step s; clamp: lines past the region's end are computed on its last line
@@ -2770,19 +2549,14 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         const pb_u32x4 h = s_img[f * NSP + min(m, NSP)];
         uint32_t o0, o1, o2, o3;
         pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
-#if PB_VL_MT
         const pb_u32x4 mm = s_m16[plo + phi]; // payload bytes [plo, phi)
         const uint32_t M0 = mm[0], M1 = mm[1], M2 = mm[2], M3 = mm[3];
-#else
-        const pb_u32x4 ml = s_m16[plo], mh = s_m16[phi];
-        const uint32_t M0 = ml[0] & ~mh[0], M1 = ml[1] & ~mh[1], M2 = ml[2] & ~mh[2], M3 = ml[3] & ~mh[3];
-#endif
         return pb_u32x4{(o0 & M0) | (h[0] & ~M0), (o1 & M1) | (h[1] & ~M1), (o2 & M2) | (h[2] & ~M2),
                         (o3 & M3) | (h[3] & ~M3)};
     };
     // steps that lie wholly inside the region: no clamp, no store guard (their four chunks' LCG
     // chains interleave instead of each running inside its own store branch)
-    const uint32_t nfull = (store && PB_VL_SPLIT) ? min(nsteps, R / PB_VL_STEP) : 0u;
+    const uint32_t nfull = min(nsteps, R / PB_VL_STEP);
     for (uint32_t s = 0; s < nfull; ++s)
     {
         pb_u32x4 v[4];
@@ -2791,7 +2565,7 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
             v[i] = chunk(s, i, false);
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
-            pb_st16_k<NT>(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
+            pb_st16_nt(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
     }
     for (uint32_t s = nfull; s < nsteps; ++s)
     {
@@ -2804,12 +2578,12 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         for (uint32_t i = 0; i < 4; ++i)
         {
             const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
-            if (store && c0 < R)
-                pb_st16_k<NT>(gout + c0, v[i]);
+            if (c0 < R)
+                pb_st16_nt(gout + c0, v[i]);
         }
     }
     if (tid == 0) // the workgroup stores exactly [lo, hi) (the launch's last chunk zero-padded)
-        pb_count(K, bxr, nown, store ? hi_abs - lo_abs : 0ull);
+        pb_count(K, bxr, nown, hi_abs - lo_abs);
 }
 
 // ---------------- variable length: lengths -> offsets -> tile map ----------------
@@ -2996,7 +2770,7 @@ __global__ __launch_bounds__(256) void pb_fillreg_kernel(pb_u32x4 *dst, uint64_t
 // 6.2 instead of 8.2 KiB, 26 instead of 19 workgroups per CU)
 static size_t pb_small_tile_bytes(uint32_t wgt, uint32_t flen)
 {
-    return PB_SMALL_DYN ? (((size_t)wgt * flen + 15) & ~(size_t)15) + 32 : 0;
+    return (((size_t)wgt * flen + 15) & ~(size_t)15) + 32;
 }
 
 // pb_small_kernel: workgroup b builds frames [wgt b, wgt b + wgt)
@@ -3006,10 +2780,7 @@ static void pbk_launch_linear(const pb_kargs *K, hipStream_t st)
     const uint32_t wgt = K->small_wgt ? K->small_wgt : PB_WG;
     const dim3 g((uint32_t)((K->n_frames + wgt - 1) / wgt));
     const size_t lds = pb_small_tile_bytes(wgt, K->fixed_len) + K->lds_pad;
-    constexpr bool NT = PB_SX_NT != 0;
-    if (K->store_flip && wgt == 64) // (experiments) the other store kind
-        hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, RANDOM, 64, AL, !NT>), g, dim3(64), lds, st, *K);
-    else if (wgt == 64)
+    if (wgt == 64)
         hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, RANDOM, 64, AL>), g, dim3(64), lds, st, *K);
     else if (wgt == 128)
         hipLaunchKernelGGL((pb_small_kernel<NDW, PROTO, RANDOM, 128, AL>), g, dim3(128), lds, st, *K);
@@ -3107,7 +2878,7 @@ extern "C" hipError_t pbk_launch_batch(const pb_kargs *Ks, uint32_t wgt, hipStre
         A.K[j] = Ks[j];
         A.g[j] = Ks[j].xs_grid;
         grid += j < 2 ? (A.g[j] + 7u) & ~7u : A.g[j];
-        const size_t l = (size_t)(j == 0 ? wgt / 64u : Ks[j].xs_np) * PB_XREG + Ks[j].lds_pad;
+        const size_t l = (size_t)(j == 0 ? wgt / 64u : Ks[j].xs_np) * PB_XREG; // (the parts' own caps do not apply)
         lds = l > lds ? l : lds;
     }
     if (wgt == 512)
@@ -3146,7 +2917,6 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
         const uint32_t grid = (uint32_t)((K->n_frames + K->vl_wgf - 1) / K->vl_wgf);
         const size_t lds = PB_VL_LDS(K->vl_wgf, K->hl == 54 ? 5 : 4, K->vl_nl48, K->vl_nlines) + K->lds_pad;
         const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
-        constexpr bool NT = PB_VL_NT != 0;
         if (K->hl == 54)
         {
             if (l4)
@@ -3154,8 +2924,6 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
             else
                 hipLaunchKernelGGL((pb_vline_kernel<54, false>), dim3(grid), dim3(PB_WG), lds, st, *K);
         }
-        else if (K->store_flip && l4) // (experiments) the other store kind
-            hipLaunchKernelGGL((pb_vline_kernel<42, true, !NT>), dim3(grid), dim3(PB_WG), lds, st, *K);
         else
         {
             if (l4)
@@ -3172,10 +2940,7 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
 #define PB_FST(GG)                                                                                        \
     do                                                                                                    \
     {                                                                                                     \
-        constexpr bool NT = PB_FS_NT != 0;                                                                \
-        if (l4 && K->store_flip) /* (experiments) the other store kind */                                \
-            hipLaunchKernelGGL((pb_fstage_kernel<GG, true, !NT>), dim3(grid), dim3(PB_WG), lds, st, *K); \
-        else if (l4)                                                                                      \
+        if (l4)                                                                                           \
             hipLaunchKernelGGL((pb_fstage_kernel<GG, true>), dim3(grid), dim3(PB_WG), lds, st, *K);      \
         else                                                                                              \
             hipLaunchKernelGGL((pb_fstage_kernel<GG, false>), dim3(grid), dim3(PB_WG), lds, st, *K);     \

@@ -173,7 +173,7 @@ static void gb_close(void *h)
 }
 
 static const pb_builder_t gpu_builder = {gb_open, gb_load,  gb_alloc, gb_build, gb_n_frames, gb_land,
-                                         gb_land_wait, gb_reg, gb_unreg, gb_free, gb_close};
+                                         gb_land_wait, gb_reg, gb_unreg, gb_free, gb_close, pbgpu_device_count};
 static const pb_builder_t *builder = &gpu_builder;
 
 void pb_set_builder(const pb_builder_t *b)
@@ -689,23 +689,37 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
     }
     if (seq_cnt >= PB_MAX_SEQUENCES)
         return;
-    const uint16_t idx = seq_cnt++;
     const int gpus = cmd.gpus > 0 ? cmd.gpus : 1;
     /* TX threads (sequence.c:741): the sequence's `threads`, else one per GPU */
     int t_cnt = seq.threads > 0 ? seq.threads : gpus;
     if (t_cnt > PB_MAX_WORKERS - worker_cnt)
         t_cnt = PB_MAX_WORKERS - worker_cnt;
-    start_time[idx] = time(NULL);
-    shared_umem_t *shared = NULL;
+    /* refusals come before the sequence takes a slot (its counters and totals line) */
+    if (builder->device_count)
+    {
+        int n_dev = 0;
+        if (builder->device_count(&n_dev) != 0)
+            n_dev = 0;
+        if (cmd.gpu_first < 0 || cmd.gpu_first + gpus > n_dev)
+        {
+            fprintf(stderr, "[%d] --gpus %d from --gpu %d needs GPUs %d..%d; %d present: %s.\n", seq_cnt + 1, gpus,
+                    cmd.gpu_first, cmd.gpu_first, cmd.gpu_first + gpus - 1, n_dev, pbgpu_strerror(PBGPU_ENODEV));
+            last_error = PBGPU_ENODEV;
+            return;
+        }
+    }
     if (cmd.shared_umem && cmd.queue_set && t_cnt > 1 && cmd.tx && strcmp(cmd.tx, "xsk") == 0)
     {
         /* every thread on one queue: their sockets would have to share the owner's fill /
          * completion rings (pb_xsk_open); refuse instead of failing threads 1..n-1 at bind */
         fprintf(stderr, "[%d] --sharedumem with --queue binds all %d threads to queue %d: use one thread, or "
-                        "drop --queue (thread t then takes queue t).\n", idx + 1, t_cnt, cmd.queue);
+                        "drop --queue (thread t then takes queue t).\n", seq_cnt + 1, t_cnt, cmd.queue);
         last_error = PBGPU_EINVAL;
         return;
     }
+    const uint16_t idx = seq_cnt++;
+    start_time[idx] = time(NULL);
+    shared_umem_t *shared = NULL;
     if (cmd.shared_umem && t_cnt > 0)
     {
         /* one UMEM for the sequence's threads (af_xdp.c:412-428), each its own power-of-two

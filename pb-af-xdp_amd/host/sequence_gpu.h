@@ -84,6 +84,9 @@ typedef struct pb_builder
     int (*host_unregister)(void *h, void *p);
     void (*free_frames)(void *h, void *frames);
     void (*close)(void *h);
+    /* GPUs present (pbgpu_device_count); NULL: not checked.  seq_send refuses a --gpu / --gpus
+     * range past it before starting any thread. */
+    int (*device_count)(int *n);
 } pb_builder_t;
 
 void pb_set_builder(const pb_builder_t *b); /* NULL: libpbgpu */

@@ -1,0 +1,623 @@
+// r05_probe.hip — round-5 A/B probe (tool only, never linked into libpbgpu.so).
+//
+// One translation unit with the product's kernels and host shim (#included), so a probe
+// kernel can reuse the frame arithmetic (pb_small_frame, pb_small_put, ...) and a loaded
+// sequence's compiled kargs, plus:
+//   * 64-B page-kernel shapes: wave-local pages (no workgroup barrier), one-wave workgroups,
+//     persistent page walkers; decomposition variants (stores only, arithmetic only);
+//   * configs[4] fused-launch variants;
+//   * write-only fill shapes over a caller's buffer (placement study: persistent XCD-owned
+//     page walkers vs region writers).
+// Built by scripts/r05/build_probe.sh into lib/libpbprobe.so; driven by scripts/r05/probe.py.
+#include "../csrc/pbgpu_kernels.hip"
+#include "../csrc/pbgpu.cpp"
+
+namespace
+{
+
+// ---------------------------------------------------------------- 64-B page shapes
+// DIAG: 0 real frames, 1 stores only (template frames, no per-frame arithmetic),
+// 2 arithmetic only (no global stores unless a data-dependent impossible match)
+template <int DIAG>
+__device__ __forceinline__ void pr_frame64(const pb_kargs &K, uint64_t f, uint32_t (&d)[16])
+{
+    if (DIAG == 1)
+    {
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+            d[t] = K.tmpl[t] ^ (t == 5 ? (uint32_t)f : 0u);
+    }
+    else
+        pb_small_frame<16, 17, true>(K, f, d);
+}
+
+template <int DIAG>
+__device__ __forceinline__ void pr_store(const pb_kargs &K, uint8_t *p, pb_u32x4 v)
+{
+    if (DIAG == 2)
+    {
+        if (v[0] == 0x9E3779B9u && v[1] == K.seq + 0x1234567u && v[2] == 0xDEADBEEFu)
+            pb_st16_nt(p, v);
+    }
+    else
+        pb_st16_nt(p, v);
+}
+
+// The product's pb_xsmall_body (256 threads, 4 pages), with DIAG.
+template <int DIAG>
+__global__ __launch_bounds__(256) void pr_xs_body(pb_kargs K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[4 * PB_XREG / 4];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const uint32_t np = K.xs_np;
+    const uint64_t T = K.total_bytes;
+    uint32_t c0, cs;
+    if (b < K.xs_full)
+        c0 = (b >> 3) * (np * 8) + (b & 7u), cs = 8;
+    else
+        c0 = K.xs_full * np + (b - K.xs_full) * np, cs = 1;
+    {
+        const uint32_t i = tid >> 6, j = tid & 63u;
+        const uint64_t f = ((uint64_t)(c0 + i * cs) << 6) + j;
+        if (f < K.n_frames)
+        {
+            uint32_t d[16];
+            pr_frame64<DIAG>(K, f, d);
+            pb_small_put<16, true, 16>(s_tile, d, i * PB_XREG + 128 + j * 64, 64);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i)
+    {
+        const uint32_t c = c0 + i * cs;
+        const uint64_t o = (uint64_t)c * PB_XPG + 16 * tid;
+        if (i < np && c < K.xs_nch && o < T)
+        {
+            const uint32_t sl = (i * PB_XREG + 128) / 16 + tid;
+            pr_store<DIAG>(K, K.out + o, reinterpret_cast<const pb_u32x4 *>(s_tile)[pb_swz(sl)]);
+        }
+    }
+}
+
+// One wave builds and stores one 4-KiB page: frames [64 c, 64 c + 64), no workgroup barrier.
+template <int DIAG>
+__device__ __forceinline__ void pr_wave_page(const pb_kargs &K, uint32_t c, uint32_t *tile)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t T = K.total_bytes;
+    const uint64_t f = ((uint64_t)c << 6) + lane;
+    if (f < K.n_frames)
+    {
+        uint32_t d[16];
+        pr_frame64<DIAG>(K, f, d);
+        pb_small_put<16, true, 16>(tile, d, lane * 64, 64);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+    {
+        const uint32_t ch = u * 64 + lane;
+        const uint64_t o = (uint64_t)c * PB_XPG + 16 * ch;
+        if (o < T)
+            pr_store<DIAG>(K, K.out + o, reinterpret_cast<const pb_u32x4 *>(tile)[pb_swz(ch)]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier(); // the tile's reads are done before a next page overwrites it
+}
+
+// wave-local pages: wave w of workgroup b owns page ((b >> 3) * NW + w) * 8 + b % 8
+template <int WGT, int DIAG>
+__global__ __launch_bounds__(WGT) void pr_xs_wave(pb_kargs K)
+{
+    constexpr uint32_t NW = WGT / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[NW * 1024];
+    const uint32_t b = blockIdx.x, w = threadIdx.x >> 6;
+    const uint32_t c = ((b >> 3) * NW + w) * 8 + (b & 7u);
+    if (c < K.xs_nch)
+        pr_wave_page<DIAG>(K, c, s_tile + w * 1024);
+}
+
+// persistent waves: the grid (a multiple of 8 workgroups) walks the pages; wave w of workgroup
+// b (XCD x = b % 8, j = b / 8 of Wx per XCD) takes page ((t Wx + j) NW + w) 8 + x at step t
+template <int WGT, int DIAG>
+__global__ __launch_bounds__(WGT) void pr_xs_persist(pb_kargs K)
+{
+    constexpr uint32_t NW = WGT / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[NW * 1024];
+    const uint32_t b = blockIdx.x, w = threadIdx.x >> 6;
+    const uint32_t x = b & 7u, j = b >> 3, Wx = gridDim.x >> 3;
+    for (uint32_t t = 0;; ++t)
+    {
+        const uint32_t c = ((t * Wx + j) * NW + w) * 8 + x;
+        if (c >= K.xs_nch)
+            break;
+        pr_wave_page<DIAG>(K, c, s_tile + w * 1024);
+    }
+}
+
+// ---------------------------------------------------------------- configs[4] fused variants
+// the 64-B part with wave-local pages at the batch's block size (part workgroup b of nwg)
+template <int WGT>
+__device__ __forceinline__ void pr_mix_xs_part(const pb_kargs &K, uint32_t b, uint32_t *s_tile)
+{
+    constexpr uint32_t NW = WGT / 64;
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t c = ((b >> 3) * NW + w) * 8 + (b & 7u);
+    if (c < K.xs_nch)
+        pr_wave_page<0>(K, c, s_tile + w * 1024);
+}
+
+// XS: 0 the product's 64-B part body, 1 wave-local pages
+template <int WGT, int XS>
+__global__ __launch_bounds__(WGT) void pr_mix_kernel(pb_batch_args A)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];
+    const uint32_t b = blockIdx.x;
+    const uint32_t o1 = (A.g[0] + 7u) & ~7u, o2 = o1 + ((A.g[1] + 7u) & ~7u);
+    if (b < o1)
+    {
+        if (b < A.g[0])
+        {
+            if (XS)
+                pr_mix_xs_part<WGT>(A.K[0], b, s_tile);
+            else
+                pb_xsmall_body<16, 17, true, WGT>(A.K[0], b, A.g[0], s_tile);
+        }
+    }
+    else if (b < o2)
+        pb_batch_part<2, WGT>(A.K[1], b - o1, A.g[1], s_tile);
+    else
+        pb_batch_part<3, WGT>(A.K[2], b - o2, A.g[2], s_tile);
+}
+
+// the same with an SGPR budget of 80 (8 waves per SIMD admitted instead of 6)
+template <int WGT, int XS>
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pr_mix_kernel_s80(pb_batch_args A)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];
+    const uint32_t b = blockIdx.x;
+    const uint32_t o1 = (A.g[0] + 7u) & ~7u, o2 = o1 + ((A.g[1] + 7u) & ~7u);
+    if (b < o1)
+    {
+        if (b < A.g[0])
+        {
+            if (XS)
+                pr_mix_xs_part<WGT>(A.K[0], b, s_tile);
+            else
+                pb_xsmall_body<16, 17, true, WGT>(A.K[0], b, A.g[0], s_tile);
+        }
+    }
+    else if (b < o2)
+        pb_batch_part<2, WGT>(A.K[1], b - o1, A.g[1], s_tile);
+    else
+        pb_batch_part<3, WGT>(A.K[2], b - o2, A.g[2], s_tile);
+}
+
+template <int WGT>
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pr_xs_wave_s80(pb_kargs K)
+{
+    constexpr uint32_t NW = WGT / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[NW * 1024];
+    const uint32_t b = blockIdx.x, w = threadIdx.x >> 6;
+    const uint32_t c = ((b >> 3) * NW + w) * 8 + (b & 7u);
+    if (c < K.xs_nch)
+        pr_wave_page<0>(K, c, s_tile + w * 1024);
+}
+
+// the product's pb_xpage_kernel with an SGPR budget of 80
+template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4>
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pr_xpage_s80(pb_kargs K)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];
+    pb_xpage_body<NDW, PROTO, RANDOM, WGT, A4>(K, blockIdx.x, gridDim.x, s_tile);
+}
+
+// ---------------------------------------------------------------- write-only fill shapes
+// persistent XCD-owned page walker: NPP pages per step (workgroup b on XCD b % 8 takes pages
+// (m NPP + p) 8 + x, m = t Wx + j)
+template <int NPP>
+__global__ __launch_bounds__(256) void pr_fill_ppage(pb_u32x4 *dst, uint32_t nch)
+{
+    const uint32_t x = blockIdx.x & 7u, j = blockIdx.x >> 3, Wx = gridDim.x >> 3;
+    for (uint32_t t = 0;; ++t)
+    {
+        const uint32_t m = t * Wx + j;
+        if ((m * NPP) * 8 + x >= nch)
+            break;
+#pragma unroll
+        for (uint32_t p = 0; p < NPP; ++p)
+        {
+            const uint32_t c = (m * NPP + p) * 8 + x;
+            if (c < nch)
+                __builtin_nontemporal_store(pb_u32x4{c, ~c, threadIdx.x, 7u}, dst + (uint64_t)c * 256 + threadIdx.x);
+        }
+    }
+}
+
+// NP XCD-strided pages per (short-lived) workgroup, as pb_xsmall_kernel's ownership
+template <int NP>
+__global__ __launch_bounds__(256) void pr_fill_xpages(pb_u32x4 *dst, uint32_t nch)
+{
+    const uint32_t b = blockIdx.x;
+#pragma unroll
+    for (uint32_t i = 0; i < NP; ++i)
+    {
+        const uint32_t c = ((b >> 3) * NP + i) * 8 + (b & 7u);
+        if (c < nch)
+            dst[(uint64_t)c * 256 + threadIdx.x] = pb_u32x4{c, ~c, threadIdx.x, 7u};
+    }
+}
+
+// persistent dense window in natural order: step t, workgroup b writes chunk t G + b of CH KiB
+template <int CH>
+__global__ __launch_bounds__(256) void pr_fill_pchunk(pb_u32x4 *dst, uint64_t n16)
+{
+    constexpr uint32_t PER = CH / 4; // 16-B stores per lane per chunk
+    for (uint64_t ck = blockIdx.x;; ck += gridDim.x)
+    {
+        const uint64_t base = ck * (uint64_t)(CH * 64);
+        if (base >= n16)
+            break;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; ++i)
+        {
+            const uint64_t c = base + i * 256 + threadIdx.x;
+            if (c < n16)
+                dst[c] = pb_u32x4{(uint32_t)c, 1u, 2u, 3u};
+        }
+    }
+}
+
+// wave-local fills: wave w of workgroup b writes unit u (u16 16-B chunks) as consecutive 1-KiB
+// store instructions; MODE 0: u = 4 b + w (natural), 1: XCD-strided ((b >> 3) 4 + w) 8 + b % 8,
+// 2: XCD-contiguous regions of 4 units (pb_xcd_region(b) 4 + w)
+template <int MODE>
+__global__ __launch_bounds__(256) void pr_fill_wave(pb_u32x4 *dst, uint64_t n16, uint32_t u16, uint32_t nunits)
+{
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u, b = blockIdx.x;
+    const uint32_t u = MODE == 0 ? b * 4 + w : (MODE == 1 ? ((b >> 3) * 4 + w) * 8 + (b & 7u) : pb_xcd_region(b, gridDim.x) * 4 + w);
+    if (u >= nunits)
+        return;
+    const uint64_t base = (uint64_t)u * u16;
+    for (uint32_t c = lane; c < u16; c += 64)
+    {
+        const uint64_t i = base + c;
+        if (i < n16)
+            __builtin_nontemporal_store(pb_u32x4{u, c, lane, 9u}, dst + i);
+    }
+}
+
+__global__ __launch_bounds__(256) void pr_cmp(const uint32_t *a, const uint32_t *b, uint64_t n, unsigned long long *bad)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        if (a[i] != b[i])
+            atomicAdd(bad, 1ull);
+}
+
+const char *const FILL_NAMES[] = {
+    "4KiB/wg natural (8/CU)",                  // 0
+    "208KiB region/wg XCD-contig 5/CU (vline)", // 1
+    "96KiB region/wg XCD-contig (fstage)",     // 2
+    "persistent XCD pages, 1/step",            // 3
+    "persistent XCD pages, 2/step",            // 4
+    "persistent XCD pages, 4/step",            // 5
+    "24KiB chunk/wg natural",                  // 6
+    "24KiB chunk/wg XCD-contig",               // 7
+    "6 XCD-strided pages/wg",                  // 8
+    "4 XCD-strided pages/wg",                  // 9
+    "persistent natural 16KiB chunks",         // 10
+    "persistent natural 4KiB chunks",          // 11
+    "16KiB/wg natural",                        // 12
+};
+constexpr int N_FILL = sizeof(FILL_NAMES) / sizeof(FILL_NAMES[0]);
+
+hipError_t pr_launch_fill(void *dst, uint64_t bytes, int shape, uint32_t pgrid, hipStream_t st)
+{
+    const uint64_t n16 = bytes / 16;
+    const uint32_t nch = (uint32_t)(n16 / 256);
+    pb_u32x4 *d = (pb_u32x4 *)dst;
+    switch (shape)
+    {
+    case 0: hipLaunchKernelGGL((pb_fill_kernel<false, 1>), dim3((uint32_t)((n16 + 255) / 256)), dim3(256), 0, st, d, n16, 5u); break;
+    case 1: hipLaunchKernelGGL((pb_fillreg_kernel<208>), dim3((uint32_t)((n16 + 208 * 64 - 1) / (208 * 64))), dim3(256), 32768, st, d, n16, 5u); break;
+    case 2: hipLaunchKernelGGL((pb_fill_kernel<false, 24, true>), dim3((uint32_t)((n16 + 24 * 256 - 1) / (24 * 256))), dim3(256), 0, st, d, n16, 5u); break;
+    case 3: hipLaunchKernelGGL((pr_fill_ppage<1>), dim3(pgrid), dim3(256), 0, st, d, nch); break;
+    case 4: hipLaunchKernelGGL((pr_fill_ppage<2>), dim3(pgrid), dim3(256), 0, st, d, nch); break;
+    case 5: hipLaunchKernelGGL((pr_fill_ppage<4>), dim3(pgrid), dim3(256), 0, st, d, nch); break;
+    case 6: hipLaunchKernelGGL((pb_fill_kernel<false, 6>), dim3((uint32_t)((n16 + 1535) / 1536)), dim3(256), 0, st, d, n16, 5u); break;
+    case 7: hipLaunchKernelGGL((pb_fill_kernel<false, 6, true>), dim3((uint32_t)((n16 + 1535) / 1536)), dim3(256), 0, st, d, n16, 5u); break;
+    case 8: hipLaunchKernelGGL((pr_fill_xpages<6>), dim3((nch + 47) / 48 * 8), dim3(256), 0, st, d, nch); break;
+    case 9: hipLaunchKernelGGL((pr_fill_xpages<4>), dim3((nch + 31) / 32 * 8), dim3(256), 0, st, d, nch); break;
+    case 10: hipLaunchKernelGGL((pr_fill_pchunk<16>), dim3(pgrid), dim3(256), 0, st, d, n16); break;
+    case 11: hipLaunchKernelGGL((pr_fill_pchunk<4>), dim3(pgrid), dim3(256), 0, st, d, n16); break;
+    case 12: hipLaunchKernelGGL((pb_fill_kernel<false, 4>), dim3((uint32_t)((n16 + 1023) / 1024)), dim3(256), 0, st, d, n16, 5u); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// a loaded sequence's kargs for a build of [first, first + n) into out, as build_impl prepares
+// them (no count records: ctr_slots null, the ring untouched)
+int pr_kargs(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, uint32_t wgt, pb_kargs *K)
+{
+    seq_slot &S = ctx->seqs[seq];
+    const uint64_t used = S.ctr_used;
+    batch_part bp;
+    bp.st = ctx->stream;
+    bp.wgt = wgt;
+    const int rc = build_impl(ctx, seq, first, n, out, &bp);
+    S.ctr_used = used;
+    if (rc != PBGPU_OK)
+        return rc;
+    *K = bp.K;
+    // product kernels count with one atomic pair per workgroup when ctr_slots is null: into the
+    // last slot's counters, which the probe never reads (never a null counters pointer)
+    K->ctr_slots = nullptr;
+    K->counters = ctx->d_counters + PB_CTR_WORDS * (size_t)(PB_MAX_SEQUENCES - 1);
+    return PBGPU_OK;
+}
+
+template <typename F>
+int pr_time_launches(pbgpu_ctx *ctx, int reps, double *ms, F launch)
+{
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(launch());
+    HIPCHK(hipEventRecord(a, ctx->stream));
+    for (int r = 0; r < reps; ++r)
+        HIPCHK(launch());
+    HIPCHK(hipEventRecord(b, ctx->stream));
+    HIPCHK(hipEventSynchronize(b));
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *ms = t / reps;
+    return PBGPU_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int pr_fill_count(void)
+{
+    return N_FILL;
+}
+const char *pr_fill_name(int i)
+{
+    return i >= 0 && i < N_FILL ? FILL_NAMES[i] : "?";
+}
+
+int pr_fill(pbgpu_ctx *ctx, void *dst, uint64_t bytes, int shape, uint32_t pgrid, int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
+    return pr_time_launches(ctx, reps, ms, [&] { return pr_launch_fill(dst, bytes, shape, pgrid, ctx->stream); });
+}
+
+// 64-B variants of sequence `seq` (a pb_xsmall_kernel sequence) over iterations [first, first + n):
+//  0 product launch (pbk_launch_build, lds_pad as given)   1 pr_xs_body full   2 stores only
+//  3 arithmetic only   4 wave-local 256   5 wave-local 64   6 wave-local 512
+//  7 persistent 256 (pgrid workgroups)   8 persistent 64   9 wave-local 256 stores only
+//  10 wave-local 256 arithmetic only  11 wave-local 256 with 80 SGPRs  12 wave-local 64 with 80 SGPRs
+int pr_xs(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, int variant, uint32_t lds_pad,
+          uint32_t pgrid, int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr_kargs(ctx, seq, first, n, out, 256, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    PB_JOIN(ctx);
+    if (!K.xs_grid || K.xp || K.small_ndw != 16 || K.fixed_len != 64)
+        return PBGPU_EINVAL;
+    const uint32_t loaded_pad = K.lds_pad;
+    K.lds_pad = lds_pad;
+    hipStream_t st = ctx->stream;
+    const uint32_t nch = K.xs_nch;
+    auto g = [&](uint32_t nw) { return dim3((nch + 8 * nw - 1) / (8 * nw) * 8); };
+    auto launch = [&]() -> hipError_t {
+        switch (variant)
+        {
+        case 0: return pbk_launch_build(&K, st);
+        case 1: hipLaunchKernelGGL(pr_xs_body<0>, dim3(K.xs_grid), dim3(256), lds_pad, st, K); break;
+        case 2: hipLaunchKernelGGL(pr_xs_body<1>, dim3(K.xs_grid), dim3(256), lds_pad, st, K); break;
+        case 3: hipLaunchKernelGGL(pr_xs_body<2>, dim3(K.xs_grid), dim3(256), lds_pad, st, K); break;
+        case 4: hipLaunchKernelGGL((pr_xs_wave<256, 0>), g(4), dim3(256), lds_pad, st, K); break;
+        case 5: hipLaunchKernelGGL((pr_xs_wave<64, 0>), g(1), dim3(64), lds_pad, st, K); break;
+        case 6: hipLaunchKernelGGL((pr_xs_wave<512, 0>), g(8), dim3(512), lds_pad, st, K); break;
+        case 7: hipLaunchKernelGGL((pr_xs_persist<256, 0>), dim3(pgrid), dim3(256), lds_pad, st, K); break;
+        case 8: hipLaunchKernelGGL((pr_xs_persist<64, 0>), dim3(pgrid), dim3(64), lds_pad, st, K); break;
+        case 9: hipLaunchKernelGGL((pr_xs_wave<256, 1>), g(4), dim3(256), lds_pad, st, K); break;
+        case 10: hipLaunchKernelGGL((pr_xs_wave<256, 2>), g(4), dim3(256), lds_pad, st, K); break;
+        case 11: hipLaunchKernelGGL((pr_xs_wave_s80<256>), g(4), dim3(256), lds_pad, st, K); break;
+        case 12: hipLaunchKernelGGL((pr_xs_wave_s80<64>), g(1), dim3(64), lds_pad, st, K); break;
+        case 13: hipLaunchKernelGGL((pr_xs_wave<1024, 0>), g(16), dim3(1024), lds_pad, st, K); break;
+        case 14: hipLaunchKernelGGL((pr_xs_wave<128, 0>), g(2), dim3(128), lds_pad, st, K); break;
+        case 15: // the product launch as loaded (its own occupancy cap)
+        {
+            pb_kargs K2 = K;
+            K2.lds_pad = loaded_pad;
+            return pbk_launch_build(&K2, st);
+        }
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    };
+    return pr_time_launches(ctx, reps, ms, launch);
+}
+
+// configs[4] fused variants: seqs[3] of kinds 1, 2, 3 (in that order), n iterations each from
+// `first`, into outs[3]:  0 product pbk_launch_batch(512)   1 pr_mix_kernel<512, 0>
+//  2 pr_mix_kernel<512, 1> (wave-local 64-B part)   3 the same with 80 SGPRs   4 <512, 0> with 80
+//  SGPRs   5 three product launches back to back   6 pr_mix_kernel<256, 1>
+int pr_mix(pbgpu_ctx *ctx, const uint16_t *seqs, uint64_t first, uint64_t n, pbgpu_frames *const *outs, int variant,
+           int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint32_t wgt = variant == 6 ? 256u : 512u;
+    pb_kargs Ks[3], Kp[3];
+    for (int j = 0; j < 3; ++j)
+    {
+        int rc = pr_kargs(ctx, seqs[j], first, n, outs[j], wgt, &Ks[j]);
+        if (rc == PBGPU_OK)
+            rc = pr_kargs(ctx, seqs[j], first, n, outs[j], 256, &Kp[j]);
+        if (rc != PBGPU_OK)
+            return rc;
+        if (pbk_batch_kind(&Ks[j]) != j + 1)
+            return PBGPU_EINVAL;
+    }
+    PB_JOIN(ctx);
+    hipStream_t st = ctx->stream;
+    pb_batch_args A;
+    size_t lds = 0;
+    uint32_t grid = 0;
+    const bool xs_wave = variant == 2 || variant == 3 || variant == 6;
+    for (int j = 0; j < 3; ++j)
+    {
+        A.K[j] = Ks[j];
+        A.g[j] = Ks[j].xs_grid;
+        if (j == 0 && xs_wave)
+            A.g[0] = (Ks[0].xs_nch + 8 * (wgt / 64) - 1) / (8 * (wgt / 64)) * 8;
+        grid += j < 2 ? (A.g[j] + 7u) & ~7u : A.g[j];
+        const size_t l = j == 0 ? (xs_wave ? (size_t)wgt * 64 : (size_t)(wgt / 64) * PB_XREG) : (size_t)Ks[j].xs_np * PB_XREG;
+        lds = l > lds ? l : lds;
+    }
+    auto launch = [&]() -> hipError_t {
+        switch (variant)
+        {
+        case 0: return pbk_launch_batch(Ks, 512, st);
+        case 1: hipLaunchKernelGGL((pr_mix_kernel<512, 0>), dim3(grid), dim3(512), lds, st, A); break;
+        case 2: hipLaunchKernelGGL((pr_mix_kernel<512, 1>), dim3(grid), dim3(512), lds, st, A); break;
+        case 3: hipLaunchKernelGGL((pr_mix_kernel_s80<512, 1>), dim3(grid), dim3(512), lds, st, A); break;
+        case 4: hipLaunchKernelGGL((pr_mix_kernel_s80<512, 0>), dim3(grid), dim3(512), lds, st, A); break;
+        case 5:
+            for (int j = 0; j < 3; ++j)
+            {
+                const hipError_t e = pbk_launch_build(&Kp[j], st);
+                if (e != hipSuccess)
+                    return e;
+            }
+            return hipSuccess;
+        case 6: hipLaunchKernelGGL((pr_mix_kernel<256, 1>), dim3(grid), dim3(256), lds, st, A); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    };
+    return pr_time_launches(ctx, reps, ms, launch);
+}
+
+// pb_xpage_kernel sequences (60-B TCP SYN, 98-B ICMP): 0 the product launch, 1 with 80 SGPRs
+int pr_xp(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, int variant, int reps,
+          double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr_kargs(ctx, seq, first, n, out, 256, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    PB_JOIN(ctx);
+    if (!K.xs_grid || !K.xp || K.xp_wgt != 512)
+        return PBGPU_EINVAL;
+    const int kind = pbk_batch_kind(&K);
+    if (kind != 2 && kind != 3)
+        return PBGPU_EINVAL;
+    hipStream_t st = ctx->stream;
+    const size_t lds = (size_t)K.xs_np * PB_XREG;
+    auto launch = [&]() -> hipError_t {
+        if (variant == 0)
+            return pbk_launch_build(&K, st);
+        const size_t l2 = variant == 2 ? (size_t)54000 : (variant == 3 ? (size_t)82000 : lds);
+        if (kind == 2)
+            hipLaunchKernelGGL((pr_xpage_s80<16, 6, true, 512, true>), dim3(K.xs_grid), dim3(512), l2, st, K);
+        else
+            hipLaunchKernelGGL((pr_xpage_s80<32, 1, false, 512, false>), dim3(K.xs_grid), dim3(512), l2, st, K);
+        return hipGetLastError();
+    };
+    return pr_time_launches(ctx, reps, ms, launch);
+}
+
+// one product build of a loaded sequence, timed (any kernel): reps launches after one warm-up
+int pr_build(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr_kargs(ctx, seq, first, n, out, 256, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    PB_JOIN(ctx);
+    return pr_time_launches(ctx, reps, ms, [&] { return pbk_launch_build(&K, ctx->stream); });
+}
+
+// a product build with its workgroups per CU capped at per_cu by dynamic LDS (0: as loaded)
+int pr_build_cap(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, uint32_t per_cu,
+                 int reps, double *ms, uint32_t *base_lds)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr_kargs(ctx, seq, first, n, out, 256, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    PB_JOIN(ctx);
+    size_t base = 0;
+    if (K.vl)
+        base = PB_VL_LDS(K.vl_wgf, K.hl == 54 ? 5 : 4, K.vl_nl48, K.vl_nlines);
+    else if (K.fst_g)
+        base = (size_t)K.fst_nbuf * K.fst_sb + PB_FST_LDS(K.fst_wgf);
+    else
+        return PBGPU_EINVAL;
+    *base_lds = (uint32_t)base;
+    if (per_cu)
+    {
+        const size_t target = PB_LDS_PER_CU / (per_cu + 1u) + 512u;
+        K.lds_pad = target > base ? (uint32_t)(target - base) : 0u;
+    }
+    return pr_time_launches(ctx, reps, ms, [&] { return pbk_launch_build(&K, ctx->stream); });
+}
+
+int pr_fill_wave_at(pbgpu_ctx *ctx, void *dst, uint64_t bytes, int mode, uint32_t unit_bytes, uint32_t lds_pad,
+                    int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
+    const uint64_t n16 = bytes / 16;
+    const uint32_t u16 = unit_bytes / 16;
+    const uint32_t nunits = (uint32_t)((n16 + u16 - 1) / u16);
+    const uint32_t grid = mode == 1 ? (nunits + 31) / 32 * 8 : (nunits + 3) / 4;
+    return pr_time_launches(ctx, reps, ms, [&]() -> hipError_t {
+        pb_u32x4 *d = (pb_u32x4 *)dst;
+        if (mode == 0)
+            hipLaunchKernelGGL(pr_fill_wave<0>, dim3(grid), dim3(256), lds_pad, ctx->stream, d, n16, u16, nunits);
+        else if (mode == 1)
+            hipLaunchKernelGGL(pr_fill_wave<1>, dim3(grid), dim3(256), lds_pad, ctx->stream, d, n16, u16, nunits);
+        else
+            hipLaunchKernelGGL(pr_fill_wave<2>, dim3(grid), dim3(256), lds_pad, ctx->stream, d, n16, u16, nunits);
+        return hipGetLastError();
+    });
+}
+
+// mismatching dwords between two device buffers
+int pr_compare(pbgpu_ctx *ctx, const void *a, const void *b, uint64_t bytes, uint64_t *bad)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    PB_JOIN(ctx);
+    unsigned long long *d = nullptr;
+    HIPCHK(hipMalloc(&d, 8));
+    HIPCHK(hipMemsetAsync(d, 0, 8, ctx->stream));
+    hipLaunchKernelGGL(pr_cmp, dim3(4096), dim3(256), 0, ctx->stream, (const uint32_t *)a, (const uint32_t *)b,
+                       bytes / 4, d);
+    HIPCHK(hipGetLastError());
+    unsigned long long h = 0;
+    HIPCHK(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(d);
+    *bad = h;
+    return PBGPU_OK;
+}
+
+} // extern "C"

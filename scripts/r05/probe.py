@@ -1,0 +1,349 @@
+"""Round-5 A/B probe driver (lib/libpbprobe.so from tools/r05_probe.hip; tool only).
+
+python3 scripts/r05/probe.py xs|mix|place [reps]
+  xs     64-B page-kernel shapes and the decomposition (full / stores only / arithmetic only /
+         the 4-KiB fill) on one buffer, variants alternating; wave-local shapes checked
+         byte for byte against the product launch
+  mix    configs[4]'s fused-launch variants on three buffers
+  place  the packed (configs[2]) and 1500-B kernels and write-only fill shapes on several
+         large buffers alive at once (each keeps its physical placement)
+One JSON line per measurement."""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pb-af-xdp_amd")]
+import pb_configs as pc  # noqa: E402
+from pbgpu import GpuContext, Sequence  # noqa: E402
+
+LIB = os.path.join(ROOT, "pb-af-xdp_amd", "lib", "libpbprobe.so")
+what = sys.argv[1]
+REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+ctx = GpuContext(0, lib_path=LIB)
+L = ctx.lib
+D = C.c_double
+L.pr_xs.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_uint32,
+                    C.c_int, C.POINTER(D)]
+L.pr_mix.argtypes = [C.c_void_p, C.POINTER(C.c_uint16), C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p), C.c_int,
+                     C.c_int, C.POINTER(D)]
+L.pr_build.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.POINTER(D)]
+L.pr_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_uint32, C.c_int, C.POINTER(D)]
+L.pr_fill_name.restype = C.c_char_p
+L.pr_compare.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+L.pr_fill_wave_at.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
+                             C.POINTER(D)]
+L.pr_build_cap.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint32, C.c_int,
+                          C.POINTER(D), C.POINTER(C.c_uint32)]
+L.pr_xp.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_int, C.POINTER(D)]
+
+
+def ok(rc, what):
+    if rc != 0:
+        raise SystemExit(f"{what}: rc {rc}")
+
+
+def emit(d):
+    print(json.dumps(d), flush=True)
+
+
+def data_ptr(fb):
+    return fb.f.data
+
+
+def ramp(fn, secs=0.6):
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < secs:
+        fn()
+
+
+if what == "xs":
+    n = 1 << 25
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c2_udp_64")), pc.SEED_BASE)
+    fb = ctx.alloc_frames(*ctx.build_size(0, n))
+    ref = ctx.alloc_frames(*ctx.build_size(0, n))
+    ms = D()
+    # variant: (name, id, lds_pad, pgrid)
+    V = [("product", 0, 0, 0), ("product cap5", 0, 15000, 0), ("body full", 1, 0, 0), ("body stores only", 2, 0, 0),
+         ("body arith only", 3, 0, 0), ("wave256", 4, 0, 0), ("wave64", 5, 0, 0), ("wave512", 6, 0, 0),
+         ("persist256 g1024", 7, 0, 1024), ("persist256 g1536", 7, 0, 1536), ("persist64 g4096", 8, 0, 4096),
+         ("persist64 g7168", 8, 0, 7168), ("wave256 stores only", 9, 0, 0), ("wave256 arith only", 10, 0, 0),
+         ("wave256 s80", 11, 0, 0), ("wave64 s80", 12, 0, 0), ("wave256 cap5", 4, 15000, 0),
+         ("wave256 cap4", 4, 23000, 0)]
+    # parity of the real-frame shapes against the product launch
+    ok(L.pr_xs(ctx.h, 0, 5, n, ref.ptr, 0, 0, 0, 1, C.byref(ms)), "ref")
+    for name, v, pad, pg in V:
+        if "only" in name:
+            continue
+        ok(L.pr_xs(ctx.h, 0, 5, n, fb.ptr, v, pad, pg, 1, C.byref(ms)), name)
+        bad = C.c_uint64()
+        ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(fb)), C.c_void_p(data_ptr(ref)), n * 64, C.byref(bad)), "cmp")
+        emit({"check": name, "bad_dwords": bad.value})
+    ramp(lambda: L.pr_xs(ctx.h, 0, 0, n, fb.ptr, 0, 0, 0, 8, C.byref(ms)))
+    res = {name: [] for name, *_ in V}
+    fills = {"fill 4KiB/wg": 0, "fill 16KiB/wg": 12}
+    for k in fills:
+        res[k] = []
+    for r in range(REPS):
+        for name, v, pad, pg in V:
+            ok(L.pr_xs(ctx.h, 0, 0, n, fb.ptr, v, pad, pg, 20, C.byref(ms)), name)
+            res[name].append(ms.value)
+        for k, s in fills.items():
+            ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), n * 64, s, 2048, 20, C.byref(ms)), k)
+            res[k].append(ms.value)
+    for k, v in res.items():
+        s = sorted(v)
+        emit({"variant": k, "ms_med": round(s[len(s) // 2], 5), "ms_min": round(s[0], 5),
+              "tbps_med": round(n * 64 / (s[len(s) // 2] * 1e-3) / 1e12, 3), "all": [round(x, 4) for x in v]})
+    fb.free()
+    ref.free()
+
+elif what == "xs8":
+    # the 64-B shapes on NBUF 2-GiB buffers (each its own placement)
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "6"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c2_udp_64")), pc.SEED_BASE)
+    bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(nbuf)]
+    ms = D()
+    V = [("product", 0, 0), ("product cap5", 0, 15000), ("wave256", 4, 0), ("wave256 cap4", 4, 23000),
+         ("wave256 cap3", 4, 25000), ("wave512", 6, 0), ("wave512 cap2", 6, 22000), ("wave1024", 13, 0)]
+    ok(L.pr_xs(ctx.h, 0, 5, n, bufs[1].ptr, 0, 0, 0, 1, C.byref(ms)), "ref")
+    ok(L.pr_xs(ctx.h, 0, 5, n, bufs[0].ptr, 13, 0, 0, 1, C.byref(ms)), "w1024")
+    bad = C.c_uint64()
+    ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(bufs[0])), C.c_void_p(data_ptr(bufs[1])), n * 64, C.byref(bad)), "cmp")
+    emit({"check": "wave1024", "bad_dwords": bad.value})
+    ramp(lambda: L.pr_xs(ctx.h, 0, 0, n, bufs[0].ptr, 0, 0, 0, 8, C.byref(ms)))
+    for r in range(REPS):
+        for i, fb in enumerate(bufs):
+            row = {"rep": r, "buf": i, "addr": hex(data_ptr(fb))}
+            for name, v, pad in V:
+                ok(L.pr_xs(ctx.h, 0, 0, n, fb.ptr, v, pad, 0, 20, C.byref(ms)), name)
+                row[name] = round(ms.value, 5)
+            ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), n * 64, 0, 2048, 20, C.byref(ms)), "fill")
+            row["fill 4KiB/wg"] = round(ms.value, 5)
+            emit(row)
+    for fb in bufs:
+        fb.free()
+
+elif what == "xs9":
+    # occupancy of the wave-local 64-B shape (dynamic LDS caps its workgroups per CU)
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "4"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c2_udp_64")), pc.SEED_BASE)
+    bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(nbuf)]
+    ms = D()
+    # (name, variant, pad): wave256 static LDS 16 KiB; wave128 8 KiB; wave512 32 KiB
+    V = [("product as loaded", 15, 0), ("wave256 cap3", 4, 25000), ("wave256 cap2", 4, 40000), ("wave256 cap1", 4, 70000),
+         ("wave128 cap6", 14, 20000), ("wave128 cap5", 14, 25000), ("wave128 cap4", 14, 33000),
+         ("wave128 cap3", 14, 37000), ("wave512 cap1", 6, 50000), ("wave256 cap4", 4, 23000)]
+    ok(L.pr_xs(ctx.h, 0, 5, n, bufs[1].ptr, 0, 0, 0, 1, C.byref(ms)), "ref")
+    ok(L.pr_xs(ctx.h, 0, 5, n, bufs[0].ptr, 14, 0, 0, 1, C.byref(ms)), "w128")
+    bad = C.c_uint64()
+    ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(bufs[0])), C.c_void_p(data_ptr(bufs[1])), n * 64, C.byref(bad)), "cmp")
+    emit({"check": "wave128", "bad_dwords": bad.value})
+    ramp(lambda: L.pr_xs(ctx.h, 0, 0, n, bufs[0].ptr, 0, 0, 0, 8, C.byref(ms)))
+    for r in range(REPS):
+        for i, fb in enumerate(bufs):
+            row = {"rep": r, "buf": i}
+            for name, v, pad in V:
+                ok(L.pr_xs(ctx.h, 0, 0, n, fb.ptr, v, pad, 0, 20, C.byref(ms)), name)
+                row[name] = round(ms.value, 5)
+            for pad, nm in ((0, "fill 4KiB 8/CU"), (45000, "fill 4KiB 3/CU"), (36000, "fill 4KiB 4/CU")):
+                ok(L.pr_fill_wave_at(ctx.h, C.c_void_p(data_ptr(fb)), n * 64, 0, 4096, pad, 20, C.byref(ms)), nm)
+                row["wavefill " + nm] = round(ms.value, 5)
+            emit(row)
+    for fb in bufs:
+        fb.free()
+
+elif what == "wfill":
+    # wave-local fill shapes (candidate store shapes for the region kernels) on NBUF large
+    # buffers beside the packed and 1500-B kernels' own rates
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "4"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
+    ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
+    f0, b0 = ctx.build_size(0, n)
+    f1, b1 = ctx.build_size(1, n)
+    bufs = [ctx.alloc_frames(max(f0, f1), max(b0, b1)) for _ in range(nbuf)]
+    fill_bytes = 27_600_000_000 // 4096 * 4096
+    ms = D()
+    S = [("natural 4KiB 8/CU", 0, 4096, 0), ("natural 4KiB 3/CU", 0, 4096, 45000), ("xpages 4KiB 8/CU", 1, 4096, 0),
+         ("xpages 4KiB 3/CU", 1, 4096, 45000), ("natural 16.5KB 8/CU", 0, 16496, 0),
+         ("natural 16.5KB 4/CU", 0, 16496, 36000), ("natural 16.5KB 3/CU", 0, 16496, 45000),
+         ("xcdreg 16.5KB 8/CU", 2, 16496, 0), ("xcdreg 16.5KB 3/CU", 2, 16496, 45000),
+         ("natural 6KB 3/CU", 0, 6000, 45000), ("natural 8KiB 3/CU", 0, 8192, 45000),
+         ("natural 24KB 3/CU", 0, 24000, 45000), ("xcdreg 4KiB 3/CU", 2, 4096, 45000)]
+    ramp(lambda: L.pr_build(ctx.h, 1, 0, n, bufs[0].ptr, 4, C.byref(ms)))
+    for rnd in range(2):
+        for i, fb in enumerate(bufs):
+            row = {"round": rnd, "buf": i}
+            ok(L.pr_build(ctx.h, 0, 0, n, fb.ptr, 6, C.byref(ms)), "c3")
+            row["c3_ms"] = round(ms.value, 4)
+            ok(L.pr_build(ctx.h, 1, 0, n, fb.ptr, 6, C.byref(ms)), "1500")
+            row["c2_1500_ms"] = round(ms.value, 4)
+            ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), fill_bytes, 1, 2048, 4, C.byref(ms)), "reg208")
+            row["reg208"] = round(fill_bytes / (ms.value * 1e-3) / 1e12, 3)
+            for nm, mode, ub, pad in S:
+                ok(L.pr_fill_wave_at(ctx.h, C.c_void_p(data_ptr(fb)), fill_bytes, mode, ub, pad, 4, C.byref(ms)), nm)
+                row[nm] = round(fill_bytes / (ms.value * 1e-3) / 1e12, 3)
+            emit(row)
+    for fb in bufs:
+        fb.free()
+
+elif what == "capx":
+    # occupancy caps of the region kernels (packed configs[2], 1500-B) on NBUF large buffers, and the
+    # 64-B page kernel as loaded beside its probe twin
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "4"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
+    ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
+    ctx.load_sequence(2, Sequence.from_config(pc.get("c2_udp_64")), pc.SEED_BASE)
+    f0, b0 = ctx.build_size(0, n)
+    f1, b1 = ctx.build_size(1, n)
+    bufs = [ctx.alloc_frames(max(f0, f1), max(b0, b1)) for _ in range(nbuf)]
+    ms = D()
+    base = C.c_uint32()
+    ramp(lambda: L.pr_build(ctx.h, 1, 0, n, bufs[0].ptr, 4, C.byref(ms)))
+    for rnd in range(REPS):
+        for i, fb in enumerate(bufs):
+            row = {"round": rnd, "buf": i}
+            for seq, nm, caps in ((0, "c3", (0, 3, 2)), (1, "1500", (0, 4, 3, 2))):
+                for cap in caps:
+                    ok(L.pr_build_cap(ctx.h, seq, 0, n, fb.ptr, cap, 6, C.byref(ms), C.byref(base)), nm)
+                    row[f"{nm} cap{cap}"] = round(ms.value, 4)
+                row[f"{nm} base_lds"] = base.value
+            for name, v, pad in (("64B as loaded", 15, 0), ("64B wave256 cap3", 4, 25000)):
+                ok(L.pr_xs(ctx.h, 2, 0, n, fb.ptr, v, pad, 0, 20, C.byref(ms)), name)
+                row[name] = round(ms.value, 5)
+            emit(row)
+    for fb in bufs:
+        fb.free()
+
+elif what == "xp":
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "4"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c4_tcp_syn")), pc.SEED_BASE)
+    ctx.load_sequence(1, Sequence.from_config(pc.get("c5_icmp_echo")), pc.SEED_BASE)
+    bufs = [ctx.alloc_frames(*ctx.build_size(1, n)) for _ in range(nbuf)]
+    ms = D()
+    for seq in (0, 1):
+        ok(L.pr_xp(ctx.h, seq, 5, n, bufs[1].ptr, 0, 1, C.byref(ms)), "ref")
+        ok(L.pr_xp(ctx.h, seq, 5, n, bufs[0].ptr, 1, 1, C.byref(ms)), "s80")
+        bad = C.c_uint64()
+        nb = n * (60 if seq == 0 else 98)
+        ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(bufs[0])), C.c_void_p(data_ptr(bufs[1])), nb, C.byref(bad)), "cmp")
+        emit({"check": f"seq{seq} s80", "bad_dwords": bad.value})
+    ramp(lambda: L.pr_xp(ctx.h, 0, 0, n, bufs[0].ptr, 0, 8, C.byref(ms)))
+    for r in range(REPS):
+        for i, fb in enumerate(bufs):
+            row = {"rep": r, "buf": i}
+            for seq, nm in ((0, "tcp60"), (1, "icmp98")):
+                for v, vn in ((0, "product"), (1, "s80"), (2, "s80 cap2"), (3, "s80 cap1")):
+                    ok(L.pr_xp(ctx.h, seq, 0, n, fb.ptr, v, 20, C.byref(ms)), nm)
+                    row[f"{nm} {vn}"] = round(ms.value, 5)
+            emit(row)
+    for fb in bufs:
+        fb.free()
+
+elif what == "detect":
+    # can a short probe at allocation time tell a slow placement?  Region vs page fills over
+    # sub-ranges of each buffer, beside the packed and 1500-B kernels' own rates; ALLOCS
+    # allocation rounds (all buffers freed in between)
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "4"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
+    ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
+    f0, b0 = ctx.build_size(0, n)
+    f1, b1 = ctx.build_size(1, n)
+    ms = D()
+    for alloc in range(int(os.environ.get("ALLOCS", "3"))):
+        bufs = [ctx.alloc_frames(max(f0, f1), max(b0, b1)) for _ in range(nbuf)]
+        if alloc == 0:
+            ramp(lambda: L.pr_build(ctx.h, 1, 0, n, bufs[0].ptr, 4, C.byref(ms)))
+        for i, fb in enumerate(bufs):
+            row = {"alloc": alloc, "buf": i, "addr": hex(data_ptr(fb))}
+            ok(L.pr_build(ctx.h, 0, 0, n, fb.ptr, 6, C.byref(ms)), "c3")
+            row["c3_ms"] = round(ms.value, 4)
+            ok(L.pr_build(ctx.h, 1, 0, n, fb.ptr, 6, C.byref(ms)), "1500")
+            row["c2_1500_ms"] = round(ms.value, 4)
+            for gb in (1, 4, 16):
+                nb = gb << 30
+                r = {}
+                for s_, nm in ((0, "page"), (1, "reg208"), (2, "reg96")):
+                    ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), nb, s_, 2048, 10 if gb < 16 else 4, C.byref(ms)), nm)
+                    r[nm] = round(nb / (ms.value * 1e-3) / 1e12, 3)
+                r["ratio208"] = round(r["reg208"] / r["page"], 3)
+                row[f"{gb}GiB"] = r
+            emit(row)
+        for fb in bufs:
+            fb.free()
+
+elif what == "mix":
+    n = 1 << 24
+    names = ["c2_udp_64", "c4_tcp_syn", "c5_icmp_echo"]
+    for i, nm in enumerate(names):
+        ctx.load_sequence(i, Sequence.from_config(pc.get(nm)), pc.SEED_BASE)
+    bufs = [ctx.alloc_frames(*ctx.build_size(i, n)) for i in range(3)]
+    refs = [ctx.alloc_frames(*ctx.build_size(i, n)) for i in range(3)]
+    seqs = (C.c_uint16 * 3)(0, 1, 2)
+    outs = (C.c_void_p * 3)(*[C.cast(b.ptr, C.c_void_p) for b in bufs])
+    routs = (C.c_void_p * 3)(*[C.cast(b.ptr, C.c_void_p) for b in refs])
+    ms = D()
+    V = [("product fused 512", 0), ("mix 512 product parts", 1), ("mix 512 wave-local 64B", 2),
+         ("mix 512 wave-local 64B s80", 3), ("mix 512 product parts s80", 4), ("three launches", 5),
+         ("mix 256 wave-local 64B", 6)]
+    ok(L.pr_mix(ctx.h, seqs, 3, n, routs, 5, 1, C.byref(ms)), "ref")
+    for name, v in V:
+        ok(L.pr_mix(ctx.h, seqs, 3, n, outs, v, 1, C.byref(ms)), name)
+        bad = 0
+        for i in range(3):
+            b = C.c_uint64()
+            nb = n * int(bufs[i].f.fixed_len)
+            ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(bufs[i])), C.c_void_p(data_ptr(refs[i])), nb, C.byref(b)),
+               "cmp")
+            bad += b.value
+        emit({"check": name, "bad_dwords": bad})
+    ramp(lambda: L.pr_mix(ctx.h, seqs, 0, n, outs, 0, 8, C.byref(ms)))
+    res = {name: [] for name, _ in V}
+    for r in range(REPS):
+        for name, v in V:
+            ok(L.pr_mix(ctx.h, seqs, 0, n, outs, v, 20, C.byref(ms)), name)
+            res[name].append(ms.value)
+    tot = sum(n * int(b.f.fixed_len) for b in bufs)
+    for k, v in res.items():
+        s = sorted(v)
+        emit({"variant": k, "ms_med": round(s[len(s) // 2], 5), "ms_min": round(s[0], 5),
+              "tbps_med": round(tot / (s[len(s) // 2] * 1e-3) / 1e12, 3), "all": [round(x, 4) for x in v]})
+    for b in bufs + refs:
+        b.free()
+
+elif what == "place":
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "4"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
+    ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
+    f0, b0 = ctx.build_size(0, n)
+    f1, b1 = ctx.build_size(1, n)
+    bufs = [ctx.alloc_frames(max(f0, f1), max(b0, b1)) for _ in range(nbuf)]
+    nfill = L.pr_fill_count()
+    fill_bytes = 27_600_000_000 // 4096 * 4096
+    ms = D()
+    ramp(lambda: L.pr_build(ctx.h, 1, 0, n, bufs[0].ptr, 4, C.byref(ms)))
+    for rnd in range(int(os.environ.get("ROUNDS", "2"))):
+        for i, fb in enumerate(bufs):
+            row = {"round": rnd, "buf": i, "addr": hex(data_ptr(fb))}
+            ok(L.pr_build(ctx.h, 0, 0, n, fb.ptr, 10, C.byref(ms)), "c3")
+            row["c3_vline_ms"] = round(ms.value, 4)
+            ok(L.pr_build(ctx.h, 1, 0, n, fb.ptr, 10, C.byref(ms)), "1500")
+            row["c2_1500_ms"] = round(ms.value, 4)
+            fills = {}
+            for s in range(nfill):
+                ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), fill_bytes, s, 2048, 5, C.byref(ms)), f"fill{s}")
+                fills[L.pr_fill_name(s).decode()] = round(fill_bytes / (ms.value * 1e-3) / 1e12, 3)
+            row["fill_tbps"] = fills
+            emit(row)
+    for fb in bufs:
+        fb.free()
+ctx.close()

@@ -163,6 +163,22 @@ void stub_install(void)
     pb_set_builder(&stub);
 }
 
+/* the stub with a device count (seq_send's up-front --gpu / --gpus check) */
+static int g_devices;
+static pb_builder_t stub_dev;
+static int s_devcount(int *n)
+{
+    *n = g_devices;
+    return 0;
+}
+void stub_set_devices(int n)
+{
+    g_devices = n;
+    stub_dev = stub;
+    stub_dev.device_count = s_devcount;
+    pb_set_builder(&stub_dev);
+}
+
 void stub_uninstall(void)
 {
     pb_set_builder(NULL);

@@ -109,11 +109,37 @@ def test_batch_fallback_sets(seqs, monkeypatch):
         assert ctx.kernel_time()[1] == 3
         _oracle_check(seqs[1], 1, 9, n, bufs[1])
         _oracle_check(seqs[1], 3, 9, n, bufs[3])
-        monkeypatch.setenv("PBGPU_BATCH", "0")
+        monkeypatch.setenv("PBGPU_BATCH", "0")  # read when a sequence is loaded
+        _load(ctx, seqs)
         ctx.build_batch([(i, 11, n, bufs[i]) for i in range(3)])
         ctx.sync()
         assert ctx.kernel_time()[1] == 3
         for i in range(3):
             _oracle_check(seqs[i], i, 11, n, bufs[i])
         for fb in bufs:
+            fb.free()
+
+
+def test_batch_failure_leaves_counters_exact(seqs):
+    """A part that cannot be built (its buffer too small) fails the whole call before any part
+    reserves count records or is launched: the counters afterwards are exactly the earlier
+    builds' (advisor, round 4), and the next batch counts normally."""
+    n = 70001
+    with GpuContext(0) as ctx:
+        _load(ctx, seqs)
+        bufs = [ctx.alloc_frames(*ctx.build_size(i, n)) for i in range(3)]
+        small = ctx.alloc_frames(*ctx.build_size(2, n // 2))
+        ctx.build_batch([(i, 0, n, bufs[i]) for i in range(3)])
+        with pytest.raises(Exception) as e:
+            ctx.build_batch([(0, n, n, bufs[0]), (1, n, n, bufs[1]), (2, n, n, small)])
+        assert "ENOSPC" in str(e.value)
+        ctx.sync()
+        p, b = ctx.counters(3)
+        assert [int(x) for x in p] == [n] * 3
+        assert [int(x) for x in b] == [n * int(fb.f.fixed_len) for fb in bufs]
+        ctx.build_batch([(i, 2 * n, n, bufs[i]) for i in range(3)])
+        ctx.sync()
+        p, b = ctx.counters(3)
+        assert [int(x) for x in p] == [2 * n] * 3
+        for fb in bufs + [small]:
             fb.free()

@@ -44,18 +44,18 @@ SHAPES = [
      ("pb_vstage_kernel<32", "pb_stage_kernel<32", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
     # pb_vstage_kernel's lane layouts by window: fixed 8-lane groups (bit 4) and
     # no 32-lane groups (bit 5) build the same bytes as the default 32/16/8 layout
-    ("vstage_fixed8", {"PBGPU_FST_DBG": "16", "PBGPU_KERNEL": "vstage"},
+    ("vstage_fixed8", {"PBGPU_VST_SHAPE": "16", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
-    ("vstage_no32", {"PBGPU_FST_DBG": "32", "PBGPU_KERNEL": "vstage"},
+    ("vstage_no32", {"PBGPU_VST_SHAPE": "32", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
     # the other correct-output switches: workgroup edges at frame starts (lines split between
     # workgroups, masked stores at every edge), natural window order, the 3-pass offsets scan
-    ("vstage_split_edges", {"PBGPU_FST_DBG": "64", "PBGPU_KERNEL": "vstage"},
+    ("vstage_split_edges", {"PBGPU_VST_SHAPE": "64", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
-    ("vstage_no_order", {"PBGPU_FST_DBG": "256", "PBGPU_KERNEL": "vstage"},
+    ("vstage_no_order", {"PBGPU_VST_SHAPE": "256", "PBGPU_KERNEL": "vstage"},
      ("pb_vstage_kernel<", "pb_stage_kernel", "pb_fstage_kernel", "pb_xsmall_kernel", "pb_small_kernel<",
       "pb_xpage_kernel", "pb_gpf_kernel")),
     ("vstage_3pass_kb8", {"PBGPU_VST_SCAN": "3pass", "PBGPU_STAGE_KB": "8", "PBGPU_KERNEL": "vstage"},

@@ -52,21 +52,6 @@ def test_counters_count_built_frames_and_stored_bytes(ctx, name, n):
     assert stored == total, kern
 
 
-@pytest.mark.parametrize("name", ["c2_udp_1500", "c3_udp_var"])
-def test_skipped_stores_show_in_the_counters(ctx, name, monkeypatch):
-    """PBGPU_FST_DBG bit 1 builds without storing (a diagnostic): no bytes are
-    counted (and for a fixed length, whose frames are counted as stored bytes /
-    length, no frames either) — the bench's counter check then fails."""
-    n = 50000
-    _, stored_ok, total, _ = _count(ctx, name, n)
-    assert stored_ok == total
-    monkeypatch.setenv("PBGPU_FST_DBG", "2")
-    frames, stored, _, kern = _count(ctx, name, n)
-    assert frames == (0 if name == "c2_udp_1500" else n) and stored == 0, kern
-    monkeypatch.delenv("PBGPU_FST_DBG")
-    assert _count(ctx, name, n)[1] == total
-
-
 def test_rebuild_waits_for_the_queued_landing(ctx):
     """copy_to_umem_async from a buffer, then pbgpu_build into the same buffer at
     once: the landed slots hold the first build's frames (the build stream waits

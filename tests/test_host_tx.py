@@ -171,6 +171,18 @@ def test_shared_umem_socket_on_the_owners_queue_is_refused(libs):
     assert r["err"] == -22 and r["seen"] == 0 and r["pckts"] == 0
 
 
+def test_gpu_range_past_the_device_count_is_refused_up_front(libs):
+    """--gpu I --gpus N names GPUs I..I+N-1: with fewer present, seq_send refuses the sequence
+    before it takes a slot or starts a thread (pbgpu_open would fail on the missing ones
+    thread by thread); a range that fits runs."""
+    cfg = _cfg(maxpckts=64, delay=0, threads=2)
+    for gpus, first in ((3, 0), (2, 1), (1, 2)):
+        r = _run(libs, cfg, devices=2, gpus=gpus, gpu_first=first)
+        assert r["err"] == -19 and r["seen"] == 0 and r["pckts"] == 0, (gpus, first, r["err"])
+    r = _run(libs, cfg, devices=2, gpus=2)
+    assert r["err"] == 0 and r["pckts"] == 64
+
+
 # ---------------------------------------------------------------- worker loop
 
 
@@ -187,10 +199,12 @@ def _seq(cfg):
     return s
 
 
-def _run(libs, cfg, seqc=1, cap=1 << 20, **cmdkw):
+def _run(libs, cfg, seqc=1, cap=1 << 20, devices=None, **cmdkw):
     host, stub = libs
     host.pb_reset()
     stub.stub_install()
+    if devices is not None:
+        stub.stub_set_devices(devices)
     assert stub.stub_record(cap) == 0
     s = _seq(cfg)
     t0 = time.perf_counter()

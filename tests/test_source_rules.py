@@ -1,0 +1,69 @@
+"""Source rules of the product library (CPU, no build needed).
+
+* The build path never reads the environment: every PBGPU_* option is read by read_opts(), which
+  only pbgpu_open (landing / stream / batch options, into the context) and pbgpu_load_sequence
+  (kernel shapes, into the sequence's slot) call (round-4 verdict: ten getenv calls ran on every
+  pbgpu_build).
+* The A/B switches of variants measured as losing are gone from the kernels and the kargs.
+* No hidden calibration launches: pbgpu_build launches the build kernel once."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "pb-af-xdp_amd", "csrc")
+
+
+def _functions(src):
+    """{top-level function name: body} of a C++ source (brace matching, comments stripped)."""
+    src = re.sub(r"//[^\n]*", "", src)
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b([A-Za-z_]\w*)\s*\((?:[^;{}()]|\([^;{}()]*\))*\)\s*(?:const\s*)?\{", src):
+        name, i, depth = m.group(1), m.end() - 1, 0
+        if name in ("if", "for", "while", "switch", "catch"):
+            continue
+        for j in range(i, len(src)):
+            if src[j] == "{":
+                depth += 1
+            elif src[j] == "}":
+                depth -= 1
+                if depth == 0:
+                    out.setdefault(name, src[i:j + 1])
+                    break
+    return out
+
+
+def test_environment_is_read_only_by_the_options_reader():
+    src = open(os.path.join(CSRC, "pbgpu.cpp")).read()
+    fns = _functions(src)
+    readers = {n for n, body in fns.items() if "getenv" in body}
+    assert readers <= {"opt_u32", "opt_is", "read_opts", "verbose"}, readers
+    callers = {n for n, body in fns.items() if re.search(r"\bread_opts\s*\(\s*\)", body) and n != "read_opts"}
+    assert callers == {"pbgpu_open", "pbgpu_load_sequence"}, callers
+    for hot in ("build_impl", "build_check", "pbgpu_build", "pbgpu_build_batch", "batch_fusable"):
+        assert hot in fns, hot
+        assert "getenv" not in fns[hot] and "read_opts" not in fns[hot], hot
+
+
+def test_losing_variants_are_not_compiled_in():
+    k = open(os.path.join(CSRC, "pbgpu_kernels.hip")).read()
+    h = open(os.path.join(CSRC, "pb_device.h")).read()
+    c = open(os.path.join(CSRC, "pbgpu.cpp")).read()
+    gone = ["PB_COUNT", "PB_RANGE_LDS", "PB_TIMING", "PB_XS_XREMAP", "PB_SMALL_XREMAP", "PB_FST_XREMAP",
+            "PB_VST_XREMAP", "PB_VL_LATE", "PB_VL_SPLIT", "PB_VL_IMGW", "PB_VL_MT", "PB_ORB_LOG12", "PB_ORB_BIDIR",
+            "PB_SMALL_DYN", "PB_XS_NT", "PB_SX_NT", "PB_FS_NT", "PB_VL_NT", "xcd_rot", "store_flip", "fst_dbg",
+            "PBGPU_XCD_ROT", "PBGPU_STORE_FLIP", "PBGPU_ALLOC_CONTIG", "PBGPU_FST_DBG", "PBGPU_TIMING\"",
+            "PBGPU_XS_TUNE", "PBGPU_LDS_PAD", "tune_xsmall"]
+    for name in gone:
+        for label, text in (("kernels", k), ("pb_device.h", h), ("pbgpu.cpp", c)):
+            assert re.search(r"\b" + re.escape(name) + (r"\b" if name[-1].isalnum() else ""), text) is None, \
+                (name, label)
+
+
+def test_build_launches_once():
+    """build_impl's only kernel launch is the build itself (the round-4 occupancy calibration ran
+    200 hidden launches into the caller's buffer on its first large build)."""
+    fns = _functions(open(os.path.join(CSRC, "pbgpu.cpp")).read())
+    body = fns["build_impl"]
+    assert body.count("pbk_launch_build(") == 2  # span mode and per-launch timing, one each
+    assert "hipEventSynchronize" not in body and "hipStreamSynchronize(st)" in body  # (only the ring's growth)
