@@ -28,6 +28,7 @@
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st);
 extern "C" uint32_t pbk_build_grid(const pb_kargs *K);
+extern "C" size_t pbk_fpage_lds(const pb_kargs *K);
 extern "C" int pbk_batch_kind(const pb_kargs *K);
 extern "C" hipError_t pbk_launch_batch(const pb_kargs *Ks, uint32_t wgt, hipStream_t st);
 extern "C" hipError_t pbk_launch_ctr_fold(const uint32_t *slots, uint64_t n, uint32_t pairs,
@@ -81,6 +82,7 @@ enum pb_kern_force
     PBO_K_VSTAGE, // =vstage: pb_vstage_kernel for packed variable lengths
     PBO_K_NOPAGE, // =nopage: no pb_xpage_kernel (linear small kernel)
     PBO_K_LINEAR, // =linear: neither page kernel
+    PBO_K_FSTAGE, // =fstage: pb_fstage_kernel for fixed lengths > 128 B (not pb_fpage_kernel)
 };
 
 struct pb_opts
@@ -132,6 +134,7 @@ pb_opts read_opts()
                    : !strcmp(k, "vstage") ? PBO_K_VSTAGE
                    : !strcmp(k, "nopage") ? PBO_K_NOPAGE
                    : !strcmp(k, "linear") ? PBO_K_LINEAR
+                   : !strcmp(k, "fstage") ? PBO_K_FSTAGE
                                           : PBO_K_AUTO;
     o.g = opt_u32("PBGPU_G");
     if (o.g != 8 && o.g != 16 && o.g != 32 && o.g != 64)
@@ -500,6 +503,8 @@ int upload(T **dptr, const T *src, size_t n)
 // point just past the next count's boundary is the one to take.)
 #define PB_LDS_PER_CU (160u * 1024u)
 #define PB_XS_WG_PER_CU 3 // pb_xsmall_kernel
+#define PB_FP_WG_PER_CU 3 // pb_fpage_kernel
+#define PB_FP_PPW 16u     // pb_fpage_kernel: pages per wave (at most)
 uint32_t lds_cap_pad(uint32_t static_bytes, uint32_t per_cu)
 {
     const uint32_t target = PB_LDS_PER_CU / (per_cu + 1u) + 512u;
@@ -1218,6 +1223,24 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             // pb_vstage_kernel: its header word sum can be 0, where the orbit sums cannot tell a
             // zero payload sum from 0xFFFF.  PBGPU_KERNEL=vstage keeps pb_vstage_kernel.
             const bool icmp00 = proto == 1 && t[34] == 0 && t[35] == 0;
+            // the orbit prefix-sum table (pb_orbit_sum: pb_vline_kernel, pb_fpage_kernel): the 2^24-step
+            // walk runs once per process; each context uploads the result
+            auto need_orbit = [&]() -> int {
+                if (ctx->d_orbit == nullptr)
+                {
+                    static std::once_flag once;
+                    static std::vector<uint32_t> orb;
+                    static uint32_t tot = 0;
+                    std::call_once(once, [] { orb = make_orbit_table(&tot); });
+                    const int rc2 = upload(&ctx->d_orbit, orb.data(), orb.size());
+                    if (rc2 != PBGPU_OK)
+                        return rc2;
+                    ctx->orbit_tot = tot;
+                }
+                K.orbit = ctx->d_orbit;
+                K.orbit_tot = ctx->orbit_tot;
+                return PBGPU_OK;
+            };
             if (!K.fixed_len && K.gpf_rmode == 1 && !(flags & PBK_LITERAL) && !gpf_only && minf >= K.hl + 32 &&
                 maxf <= 4096 && !icmp00 && O.kernel != PBO_K_VSTAGE && O.kernel != PBO_K_STAGE)
             {
@@ -1233,24 +1256,13 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                     if (PB_VL_LDS(wf, nsp, nl48, nlines) <= 40 * 1024 || wf <= 32) // >= 4 workgroups per CU
                         break;
                 }
-                if (ctx->d_orbit == nullptr)
-                {
-                    // the 2^24-step walk runs once per process; each context uploads the result
-                    static std::once_flag once;
-                    static std::vector<uint32_t> orb;
-                    static uint32_t tot = 0;
-                    std::call_once(once, [] { orb = make_orbit_table(&tot); });
-                    int rc2 = upload(&ctx->d_orbit, orb.data(), orb.size());
-                    if (rc2 != PBGPU_OK)
-                        return rc2;
-                    ctx->orbit_tot = tot;
-                }
+                const int orc = need_orbit();
+                if (orc != PBGPU_OK)
+                    return orc;
                 K.vl = 1;
                 K.vl_wgf = wf;
                 K.vl_nl48 = nl48;
                 K.vl_nlines = nlines;
-                K.orbit = ctx->d_orbit;
-                K.orbit_tot = ctx->orbit_tot;
             }
             if (fst_ok)
             {
@@ -1278,6 +1290,21 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                     }
                     if (K.fst_g)
                         break;
+                }
+                // one wave per XCD-owned page (pb_fpage_kernel) unless a pb_fstage_kernel shape is
+                // asked for; pb_fstage_kernel stays the form for buffers that are not 4-KiB aligned
+                if (K.fst_g && !icmp00 && O.kernel != PBO_K_FSTAGE && !eg && !ew && !en)
+                {
+                    const int orc = need_orbit();
+                    if (orc != PBGPU_OK)
+                        return orc;
+                    K.fp = 1;
+                    K.fp_nf = 4096 / minf + 2;
+                    K.fp_ppw = std::max(1u, std::min(PB_FP_PPW, 64u / K.fp_nf));
+                    K.xs_np = PB_WG / 64 * K.fp_ppw; // pages per workgroup
+                    K.vl_nl48 = (maxf + 31) / 16 + 1;
+                    K.xp_inv = 1.0 / (double)minf;
+                    K.lds_pad = lds_cap_pad((uint32_t)pbk_fpage_lds(&K), PB_FP_WG_PER_CU);
                 }
             }
         }
@@ -1575,18 +1602,18 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
     K.xs_grid = 0;
     if (bp && K.small_ndw && K.xs_np && !K.xp) // pb_batch_kernel's 64-B part at the batch's block size
         K.xs_np = bp->wgt >> K.xs_fp_shift;
-    if (K.small_ndw && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && S.opt.kernel != PBO_K_LINEAR)
+    if ((K.small_ndw || K.fp) && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && S.opt.kernel != PBO_K_LINEAR)
     {
-        // XCD-owned 4 KiB pages, xs_np per workgroup: pb_xsmall_kernel (one wave per page) takes
-        // groups of 8 workgroups (pages past the stream are skipped); pb_xpage_kernel and the
-        // batch's 64-B part take full groups of 8, then the tail pages in order
+        // XCD-owned 4 KiB pages, xs_np per workgroup: pb_xsmall_kernel and pb_fpage_kernel (one
+        // wave per page) take groups of 8 workgroups (pages past the stream are skipped);
+        // pb_xpage_kernel and the batch's 64-B part take full groups of 8, then the tail pages in order
         const uint64_t nch = (K.total_bytes + 4095) / 4096;
         if (nch < 0x7FFFFFFFull)
         {
             K.xs_nch = (uint32_t)nch;
             const uint32_t np = K.xs_np;
             K.xs_full = (uint32_t)(nch / (8 * np) * 8);
-            if (K.xp || bp)
+            if (K.xp || (bp && K.small_ndw))
                 K.xs_grid = K.xs_full + (uint32_t)((nch - (uint64_t)K.xs_full * np + np - 1) / np);
             else
                 K.xs_grid = (uint32_t)((nch + 8ull * np - 1) / (8ull * np) * 8);
@@ -2353,7 +2380,9 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
     if (!S.loaded)
         return PBGPU_ENOENT;
     const pb_kargs &K = S.K;
-    if (K.vl)
+    if (K.fp) // (pb_fstage_kernel for a frames buffer that is not 4-KiB aligned)
+        snprintf(buf, n, "pb_fpage_kernel<%u, %u>", K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
+    else if (K.vl)
         snprintf(buf, n, "pb_vline_kernel<%u, %u>", K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
     else if (K.fst_g)
         snprintf(buf, n, "pb_fstage_kernel<%u, %u>", K.fst_g, (K.flags & PBK_L4_CSUM) ? 1u : 0u);

@@ -120,6 +120,25 @@ __global__ __launch_bounds__(WGT) void pr_xs_wave(pb_kargs K)
         pr_wave_page<DIAG>(K, c, s_tile + w * 1024);
 }
 
+// pr_xs_wave with a per-workgroup count record (a plain store, as the product's ring) or atomic
+template <int WGT, int CNT>
+__global__ __launch_bounds__(WGT) void pr_xs_wave_cnt(pb_kargs K, uint32_t *slots)
+{
+    constexpr uint32_t NW = WGT / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[NW * 1024];
+    const uint32_t b = blockIdx.x, w = threadIdx.x >> 6;
+    const uint32_t c = ((b >> 3) * NW + w) * 8 + (b & 7u);
+    if (c < K.xs_nch)
+        pr_wave_page<0>(K, c, s_tile + w * 1024);
+    if (threadIdx.x == 0)
+    {
+        if (CNT == 1)
+            slots[pb_xcd_region(b, gridDim.x)] = NW * 4096u;
+        else
+            atomicAdd(reinterpret_cast<unsigned long long *>(slots) + (b % 64) * 16, (unsigned long long)NW * 4096u);
+    }
+}
+
 // persistent waves: the grid (a multiple of 8 workgroups) walks the pages; wave w of workgroup
 // b (XCD x = b % 8, j = b / 8 of Wx per XCD) takes page ((t Wx + j) NW + w) 8 + x at step t
 template <int WGT, int DIAG>
@@ -416,6 +435,14 @@ int pr_xs(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames
     PB_JOIN(ctx);
     if (!K.xs_grid || K.xp || K.small_ndw != 16 || K.fixed_len != 64)
         return PBGPU_EINVAL;
+    static uint32_t *scratch = nullptr; // count records of the probe's counting variants (1 MiB)
+    if (scratch == nullptr)
+    {
+        HIPCHK(hipMalloc((void **)&scratch, 1u << 20));
+        HIPCHK(hipMemset(scratch, 0, 1u << 20));
+    }
+    if (K.xs_grid > (1u << 18))
+        return PBGPU_EINVAL;
     const uint32_t loaded_pad = K.lds_pad;
     K.lds_pad = lds_pad;
     hipStream_t st = ctx->stream;
@@ -439,6 +466,8 @@ int pr_xs(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames
         case 12: hipLaunchKernelGGL((pr_xs_wave_s80<64>), g(1), dim3(64), lds_pad, st, K); break;
         case 13: hipLaunchKernelGGL((pr_xs_wave<1024, 0>), g(16), dim3(1024), lds_pad, st, K); break;
         case 14: hipLaunchKernelGGL((pr_xs_wave<128, 0>), g(2), dim3(128), lds_pad, st, K); break;
+        case 16: hipLaunchKernelGGL((pr_xs_wave_cnt<256, 1>), g(4), dim3(256), lds_pad, st, K, scratch); break;
+        case 17: hipLaunchKernelGGL((pr_xs_wave_cnt<256, 2>), g(4), dim3(256), lds_pad, st, K, scratch); break;
         case 15: // the product launch as loaded (its own occupancy cap)
         {
             pb_kargs K2 = K;
@@ -554,6 +583,33 @@ int pr_build(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_fra
     return pr_time_launches(ctx, reps, ms, [&] { return pbk_launch_build(&K, ctx->stream); });
 }
 
+// pb_fpage_kernel at ppw pages per wave, page order ord, capped at per_cu workgroups per CU
+int pr_fpage(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, uint32_t ppw, int ord,
+             uint32_t per_cu, int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr_kargs(ctx, seq, first, n, out, 256, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    PB_JOIN(ctx);
+    if (!K.fp || !K.xs_grid || ppw == 0 || ppw * K.fp_nf > 64 || K.hl != 42 || !(K.flags & PBK_L4_CSUM))
+        return PBGPU_EINVAL;
+    K.fp_ppw = ppw;
+    K.xs_np = 4 * ppw;
+    K.xs_grid = (uint32_t)(((uint64_t)K.xs_nch + 8ull * K.xs_np - 1) / (8ull * K.xs_np) * 8);
+    const size_t base = pbk_fpage_lds(&K);
+    const size_t target = per_cu ? PB_LDS_PER_CU / (per_cu + 1u) + 512u : 0;
+    const size_t lds = target > base ? target : base;
+    return pr_time_launches(ctx, reps, ms, [&]() -> hipError_t {
+        if (ord == 0)
+            hipLaunchKernelGGL((pb_fpage_kernel<42, true, 0>), dim3(K.xs_grid), dim3(PB_WG), lds, ctx->stream, K);
+        else
+            hipLaunchKernelGGL((pb_fpage_kernel<42, true, 1>), dim3(K.xs_grid), dim3(PB_WG), lds, ctx->stream, K);
+        return hipGetLastError();
+    });
+}
+
 // a product build with its workgroups per CU capped at per_cu by dynamic LDS (0: as loaded)
 int pr_build_cap(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, uint32_t per_cu,
                  int reps, double *ms, uint32_t *base_lds)
@@ -565,7 +621,9 @@ int pr_build_cap(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu
         return rc;
     PB_JOIN(ctx);
     size_t base = 0;
-    if (K.vl)
+    if (K.fp && K.xs_grid)
+        base = pbk_fpage_lds(&K);
+    else if (K.vl)
         base = PB_VL_LDS(K.vl_wgf, K.hl == 54 ? 5 : 4, K.vl_nl48, K.vl_nlines);
     else if (K.fst_g)
         base = (size_t)K.fst_nbuf * K.fst_sb + PB_FST_LDS(K.fst_wgf);

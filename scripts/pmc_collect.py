@@ -23,7 +23,7 @@ for d in sorted(glob.glob(os.path.join(out_dir, "pmc_*"))):
         agg = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"]
-            build = kn.startswith("void pb_") and any(x in kn for x in ("gpf", "stage", "small", "xpage", "vline", "batch"))
+            build = kn.startswith("void pb_") and any(x in kn for x in ("gpf", "stage", "small", "xpage", "vline", "batch", "fpage"))
             aux = kn.startswith("void pb_len_") or kn.startswith("pb_len_") or "pb_scan_blocks" in kn
             fold = "pb_ctr_fold" in kn  # the counters' fold: its bytes spread over the build launches
             aux = aux or fold
