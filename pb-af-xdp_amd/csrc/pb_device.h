@@ -158,12 +158,6 @@ struct pb_kargs
     // sequences, {frames, bytes} for variable ones, at position pb_xcd_region(blockIdx.x); the
     // host folds them into `counters` (pb_ctr_fold).  Null: one atomic per workgroup instead.
     uint32_t *ctr_slots;
-    // pb_fpage_kernel (fixed lengths > 128 B, one wave per XCD-owned 4-KiB page; the xs_* page grid,
-    // the orbit table and vl_nl48 lcg48 entries as pb_vline_kernel; pb_fstage_kernel's fields kept for
-    // a buffer that is not 4-KiB aligned)
-    uint32_t fp;            // 1: use it
-    uint32_t fp_nf;         // frame slots per page: 4096 / flen + 2
-    uint32_t fp_ppw;        // pages per wave (at most 64 / fp_nf: one record per lane)
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

@@ -28,7 +28,6 @@
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st);
 extern "C" uint32_t pbk_build_grid(const pb_kargs *K);
-extern "C" size_t pbk_fpage_lds(const pb_kargs *K);
 extern "C" int pbk_batch_kind(const pb_kargs *K);
 extern "C" hipError_t pbk_launch_batch(const pb_kargs *Ks, uint32_t wgt, hipStream_t st);
 extern "C" hipError_t pbk_launch_ctr_fold(const uint32_t *slots, uint64_t n, uint32_t pairs,
@@ -82,7 +81,6 @@ enum pb_kern_force
     PBO_K_VSTAGE, // =vstage: pb_vstage_kernel for packed variable lengths
     PBO_K_NOPAGE, // =nopage: no pb_xpage_kernel (linear small kernel)
     PBO_K_LINEAR, // =linear: neither page kernel
-    PBO_K_FSTAGE, // =fstage: pb_fstage_kernel for fixed lengths > 128 B (not pb_fpage_kernel)
 };
 
 struct pb_opts
@@ -134,7 +132,6 @@ pb_opts read_opts()
                    : !strcmp(k, "vstage") ? PBO_K_VSTAGE
                    : !strcmp(k, "nopage") ? PBO_K_NOPAGE
                    : !strcmp(k, "linear") ? PBO_K_LINEAR
-                   : !strcmp(k, "fstage") ? PBO_K_FSTAGE
                                           : PBO_K_AUTO;
     o.g = opt_u32("PBGPU_G");
     if (o.g != 8 && o.g != 16 && o.g != 32 && o.g != 64)
@@ -503,8 +500,6 @@ int upload(T **dptr, const T *src, size_t n)
 // point just past the next count's boundary is the one to take.)
 #define PB_LDS_PER_CU (160u * 1024u)
 #define PB_XS_WG_PER_CU 3 // pb_xsmall_kernel
-#define PB_FP_WG_PER_CU 3 // pb_fpage_kernel
-#define PB_FP_PPW 16u     // pb_fpage_kernel: pages per wave (at most)
 uint32_t lds_cap_pad(uint32_t static_bytes, uint32_t per_cu)
 {
     const uint32_t target = PB_LDS_PER_CU / (per_cu + 1u) + 512u;
@@ -1223,7 +1218,7 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             // pb_vstage_kernel: its header word sum can be 0, where the orbit sums cannot tell a
             // zero payload sum from 0xFFFF.  PBGPU_KERNEL=vstage keeps pb_vstage_kernel.
             const bool icmp00 = proto == 1 && t[34] == 0 && t[35] == 0;
-            // the orbit prefix-sum table (pb_orbit_sum: pb_vline_kernel, pb_fpage_kernel): the 2^24-step
+            // the orbit prefix-sum table (pb_orbit_sum, pb_vline_kernel): the 2^24-step
             // walk runs once per process; each context uploads the result
             auto need_orbit = [&]() -> int {
                 if (ctx->d_orbit == nullptr)
@@ -1290,21 +1285,6 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                     }
                     if (K.fst_g)
                         break;
-                }
-                // one wave per XCD-owned page (pb_fpage_kernel) unless a pb_fstage_kernel shape is
-                // asked for; pb_fstage_kernel stays the form for buffers that are not 4-KiB aligned
-                if (K.fst_g && !icmp00 && O.kernel != PBO_K_FSTAGE && !eg && !ew && !en)
-                {
-                    const int orc = need_orbit();
-                    if (orc != PBGPU_OK)
-                        return orc;
-                    K.fp = 1;
-                    K.fp_nf = 4096 / minf + 2;
-                    K.fp_ppw = std::max(1u, std::min(PB_FP_PPW, 64u / K.fp_nf));
-                    K.xs_np = PB_WG / 64 * K.fp_ppw; // pages per workgroup
-                    K.vl_nl48 = (maxf + 31) / 16 + 1;
-                    K.xp_inv = 1.0 / (double)minf;
-                    K.lds_pad = lds_cap_pad((uint32_t)pbk_fpage_lds(&K), PB_FP_WG_PER_CU);
                 }
             }
         }
@@ -1602,10 +1582,10 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
     K.xs_grid = 0;
     if (bp && K.small_ndw && K.xs_np && !K.xp) // pb_batch_kernel's 64-B part at the batch's block size
         K.xs_np = bp->wgt >> K.xs_fp_shift;
-    if ((K.small_ndw || K.fp) && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && S.opt.kernel != PBO_K_LINEAR)
+    if (K.small_ndw && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && S.opt.kernel != PBO_K_LINEAR)
     {
-        // XCD-owned 4 KiB pages, xs_np per workgroup: pb_xsmall_kernel and pb_fpage_kernel (one
-        // wave per page) take groups of 8 workgroups (pages past the stream are skipped);
+        // XCD-owned 4 KiB pages, xs_np per workgroup: pb_xsmall_kernel (one wave per page) takes
+        // groups of 8 workgroups (pages past the stream are skipped);
         // pb_xpage_kernel and the batch's 64-B part take full groups of 8, then the tail pages in order
         const uint64_t nch = (K.total_bytes + 4095) / 4096;
         if (nch < 0x7FFFFFFFull)
@@ -2380,9 +2360,7 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
     if (!S.loaded)
         return PBGPU_ENOENT;
     const pb_kargs &K = S.K;
-    if (K.fp) // (pb_fstage_kernel for a frames buffer that is not 4-KiB aligned)
-        snprintf(buf, n, "pb_fpage_kernel<%u, %u>", K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
-    else if (K.vl)
+    if (K.vl)
         snprintf(buf, n, "pb_vline_kernel<%u, %u>", K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
     else if (K.fst_g)
         snprintf(buf, n, "pb_fstage_kernel<%u, %u>", K.fst_g, (K.flags & PBK_L4_CSUM) ? 1u : 0u);

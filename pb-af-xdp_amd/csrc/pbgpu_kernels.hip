@@ -2578,192 +2578,6 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         pb_count(K, bxr, nown, hi_abs - lo_abs);
 }
 
-// ---------------- fixed lengths > 128 B, XCD-owned pages by waves: pb_fpage_kernel ----------------
-//
-// The 1500-B frames of the metric's second leg (and any fixed length > 128 B, a multiple of 4,
-// random stream payload).  pb_fstage_kernel's store shape (each workgroup 64 consecutive frames, a
-// 96-KiB region; the regions of an XCD contiguous) runs 7.0-7.1 ms per 2^25 frames in some frame
-// buffers and 7.3-8.4 ms in others, by where the buffer's pages lie; the XCD-owned
-// 4-KiB page shape of pb_xsmall_kernel does not depend on it.  Here each wave owns PPW pages
-// (K.fp_ppw, up to 64 / fp_nf), page h being c = (((b / 8) 4 + w) PPW + h) 8 + b % 8 of the packed
-// stream, whatever frames cut it:
-//  * records, for all its pages at once: lane h fp_nf + t builds frame fa_h + t of page h (the
-//    frames touching a page: at most 4096 / flen + 2): seed, fields, header image with both
-//    checksums (the L4 payload sum from the orbit prefix sums, pb_orbit_sum, as pb_vline_kernel),
-//    the record {first chunk, payload start, end, LCG state at its first chunk} and the header
-//    shifted to its byte position, in the wave's LDS slots (positions relative to the page).  One
-//    record per lane: the setup's latency chain (seed, discrete log, orbit-table loads) is paid
-//    once for PPW pages (at one page per wave it was: 13.5-16.4 ms per 2^25 1500-B frames);
-//  * chunks: per page, lane l stores chunks l, l + 64, l + 128, l + 192 (four 1-KiB store
-//    instructions per wave): the frame holding the chunk's first byte is (16 ci + r_h) / flen, its
-//    record gives the chunk's payload and header bytes (pb_vline_kernel's chunk machinery).
-// The frames cut by a page edge are set up by both pages' lanes (their records only: every byte is
-// generated and stored once).  One workgroup barrier (the shared tables), none after.
-// ORD 0: the wave's pages are consecutive in its XCD's class (c = (m0 + h) 8 + x); 1: page h of
-// every wave of the launch before page h + 1 (c = ((h G8 + b / 8) 4 + w) 8 + x, G8 = grid / 8)
-template <int HL, bool L4, int ORD = 0>
-__global__ __launch_bounds__(PB_WG) void pb_fpage_kernel(pb_kargs K)
-{
-    constexpr uint32_t NSP = (15 + HL + 15) / 16; // chunks a frame's header can touch
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-    uint2 *const s_jt = reinterpret_cast<uint2 *>(s_dyn);              // jump[PB_JNEG - (i + HL)], i < 16
-    pb_u32x4 *const s_m16 = reinterpret_cast<pb_u32x4 *>(s_dyn + 32);  // byte masks by plo + phi
-    uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_m16 + PB_VL_NMASK); // L^(48 m), m < vl_nl48
-    const uint32_t NF = K.fp_nf, PPW = K.fp_ppw; // frame slots per page, pages per wave
-    const uint32_t PSL = NF * (1 + NSP) + 1;     // 16-B LDS slots per page: records, images, a zero chunk
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    pb_u32x4 *const s_wave = reinterpret_cast<pb_u32x4 *>(s_l48 + ((K.vl_nl48 + 1u) & ~1u)) + w * PPW * PSL;
-    if (tid < 16u)
-        s_jt[tid] = K.jump[PB_JNEG - (tid + HL)];
-    if (tid <= 32u)
-    {
-        const int lo = tid > 16u ? (int)tid - 16 : 0, hi = tid > 16u ? 16 : (int)tid;
-        s_m16[tid] = pb_u32x4{pb_range_mask(lo, hi), pb_range_mask(lo - 4, hi - 4), pb_range_mask(lo - 8, hi - 8),
-                              pb_range_mask(lo - 12, hi - 12)};
-    }
-    for (uint32_t i = tid; i < K.vl_nl48; i += PB_WG)
-        s_l48[i] = K.lcg48[i];
-    __syncthreads();
-
-    const uint32_t b = blockIdx.x, flags = K.flags;
-    const uint32_t flen = K.fixed_len;
-    const uint64_t T = K.total_bytes;
-    // page h of the wave: c, the frame holding its byte 0 (fa), that frame's bytes before it (r),
-    // the frames touching it (nf, 0 past the stream)
-    auto page_of = [&](uint32_t h, uint32_t wv) -> uint32_t {
-        return ORD == 0 ? (((b >> 3) * 4 + wv) * PPW + h) * 8 + (b & 7u)
-                        : ((h * (gridDim.x >> 3) + (b >> 3)) * 4 + wv) * 8 + (b & 7u);
-    };
-    auto page = [&](uint32_t h, uint64_t &fa, uint32_t &r, uint32_t &nf) -> uint32_t {
-        const uint32_t c = page_of(h, w);
-        fa = 0, r = 0, nf = 0;
-        if (c < K.xs_nch)
-        {
-            fa = pb_xp_first_frame64(c, flen, K.xp_inv);
-            r = (uint32_t)((uint64_t)c * PB_XPG - fa * flen);
-            nf = (uint32_t)min((uint64_t)pb_divq(r + PB_XPG - 1u, K.flen) + 1u, K.n_frames - fa);
-        }
-        return c;
-    };
-    // ---------------- records: lane h NF + t, frame t of page h ----------------
-    {
-        const uint32_t h = lane / NF, t = lane - h * NF;
-        uint64_t fa;
-        uint32_t r, nf;
-        if (h < PPW)
-            page(h, fa, r, nf);
-        else
-            nf = 0;
-        pb_u32x4 *const s_rec = s_wave + h * PSL, *const s_img = s_rec + NF;
-        if (t < nf)
-        {
-            const uint64_t f = fa + t;
-            const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + f);
-            const uint32_t r0 = pb_rand_r(s);
-            const pb_frame_pl P = pb_payload<false>(K, s, 0);
-            uint32_t d[16];
-            const uint32_t l4tot = pb_header(K, r0, P.plen, d, pb_range(K, r0));
-            if (L4)
-            {
-                // csum_tcpudp_magic / icmp_csum (sequence.c:569-594): header (+ pseudo header) words
-                // plus the payload's, from the orbit prefix sums
-                uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) + pb_halves(d[12]) +
-                              pb_halves(d[13]);
-                if (flags & PBK_PSEUDO)
-                    hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
-                const uint32_t cs = (~pb_fold(pb_fold(hs) + pb_orbit_sum(K, P.st0, P.plen))) & 0xFFFFu;
-#pragma unroll
-                for (uint32_t u = 0; u < 16; ++u)
-                    d[u] |= u == K.csum_dw ? (K.csum_hi ? (cs << 16) : cs) : 0u;
-            }
-            // the frame's start relative to the page (frame 0's may be before it)
-            const int32_t st = (int32_t)(t * flen) - (int32_t)r;
-            const uint32_t s0 = (uint32_t)st & 15u;
-            const uint2 jt = s_jt[s0];
-            s_rec[t] = pb_u32x4{(uint32_t)(st >> 4), (uint32_t)(st + HL), (uint32_t)(st + (int32_t)flen),
-                                jt.x * P.st0 + jt.y};
-            // the header image shifted to byte s0 of the frame's first chunk (out dword u: image bytes
-            // [4u - s0, 4u - s0 + 4)); only its header bytes are ever read
-            const uint32_t q = s0 >> 2, sh = s0 & 3u;
-            uint32_t v[17];
-#pragma unroll
-            for (int u = 0; u < 17; ++u)
-            {
-                const uint32_t lo = u > 0 ? d[u - 1] : 0u, hi = u < 16 ? d[u] : 0u;
-                v[u] = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
-            }
-            constexpr uint32_t NHW = (HL + 6) / 4;
-            static_assert(3 + NHW <= 4 * NSP, "image slot");
-            uint32_t *const img32 = reinterpret_cast<uint32_t *>(s_img + t * NSP) + q;
-#pragma unroll
-            for (uint32_t u = 0; u < NHW; ++u)
-                img32[u] = v[u];
-        }
-        if (h < PPW && t == 0u) // the chunk after the page's last frame's: no frame starts there
-            s_img[nf * NSP] = pb_u32x4{0u, 0u, 0u, 0u};
-    }
-    // the wave's records before its chunks (a wave's LDS operations complete in order)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---------------- chunks, page by page ----------------
-    for (uint32_t h = 0; h < PPW; ++h)
-    {
-        uint64_t fa;
-        uint32_t r, nf;
-        const uint32_t c = page(h, fa, r, nf);
-        if (nf == 0u)
-        {
-            if (ORD == 0)
-                break; // (pages in order: the rest are past the stream too)
-            continue;
-        }
-        const pb_u32x4 *const s_rec = s_wave + h * PSL, *const s_img = s_rec + NF;
-        const uint64_t P0 = (uint64_t)c * PB_XPG;
-        pb_u32x4 v[4];
-#pragma unroll
-        for (uint32_t u = 0; u < 4; ++u)
-        {
-            const uint32_t ci = u * 64 + lane;
-            // the frame holding the chunk's first byte (chunks past the stream's end, never stored,
-            // read the last frame's record)
-            const uint32_t t = min(pb_divq(16 * ci + r, K.flen), nf - 1u);
-            const pb_u32x4 rc = s_rec[t];
-            const uint32_t m = min(ci - rc[0], K.vl_nl48 - 1u); // chunk index within frame t
-            const uint2 L = s_l48[m];
-            const uint32_t x = __umul24(rc[3], L.x) + L.y;
-            const int32_t pb = (int32_t)(ci << 4);
-            const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
-            const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
-            const pb_u32x4 hd = s_img[t * NSP + min(m, NSP)];
-            uint32_t o0, o1, o2, o3;
-            pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
-            const pb_u32x4 mm = s_m16[plo + phi]; // payload bytes [plo, phi)
-            v[u] = pb_u32x4{(o0 & mm[0]) | (hd[0] & ~mm[0]), (o1 & mm[1]) | (hd[1] & ~mm[1]),
-                            (o2 & mm[2]) | (hd[2] & ~mm[2]), (o3 & mm[3]) | (hd[3] & ~mm[3])};
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < 4; ++u)
-        {
-            const uint64_t o = P0 + 16 * (u * 64 + lane);
-            if (o < T)
-                pb_st16_nt(K.out + o, v[u]);
-        }
-    }
-    if (tid == 0)
-    {
-        // the workgroup's stored bytes (fixed length: frames = bytes / length on the host)
-        uint64_t by = 0;
-        for (uint32_t i = 0; i < 4 * PPW; ++i)
-        {
-            const uint32_t ci = page_of(i % PPW, i / PPW);
-            if (ci < K.xs_nch)
-                by += min((uint64_t)PB_XPG, T - (uint64_t)ci * PB_XPG);
-        }
-        pb_count_at(K, b, pb_xcd_region(b, gridDim.x), 0, by);
-    }
-}
-
 // ---------------- variable length: lengths -> offsets -> tile map ----------------
 
 __global__ __launch_bounds__(256) void pb_len_reduce(pb_kargs K, unsigned long long *block_sums)
@@ -3073,8 +2887,6 @@ extern "C" uint32_t pbk_build_grid(const pb_kargs *K)
 {
     const uint64_t n = K->n_frames;
     uint64_t per = 0;
-    if (K->fp && K->xs_grid)
-        return K->xs_grid;
     if (K->vl)
         per = K->vl_wgf;
     else if (K->fst_g)
@@ -3090,35 +2902,9 @@ extern "C" uint32_t pbk_build_grid(const pb_kargs *K)
     return per ? (uint32_t)((n + per - 1) / per) : 0u;
 }
 
-// pb_fpage_kernel's LDS: the shared tables, then per page of each wave fp_nf records + fp_nf * NSP
-// image chunks + a zero chunk
-extern "C" size_t pbk_fpage_lds(const pb_kargs *K)
-{
-    const size_t nsp = K->hl == 54 ? 5 : 4;
-    return 128 + (size_t)PB_VL_NMASK * 16 + (size_t)((K->vl_nl48 + 1u) & ~1u) * 8 +
-           (size_t)(PB_WG / 64) * K->fp_ppw * ((size_t)K->fp_nf * (1 + nsp) + 1) * 16;
-}
-
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
 {
-    if (K->fp && K->xs_grid)
-    {
-        const size_t lds = pbk_fpage_lds(K) + K->lds_pad;
-        const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
-        const dim3 g(K->xs_grid);
-        if (K->hl == 54)
-        {
-            if (l4)
-                hipLaunchKernelGGL((pb_fpage_kernel<54, true>), g, dim3(PB_WG), lds, st, *K);
-            else
-                hipLaunchKernelGGL((pb_fpage_kernel<54, false>), g, dim3(PB_WG), lds, st, *K);
-        }
-        else if (l4)
-            hipLaunchKernelGGL((pb_fpage_kernel<42, true>), g, dim3(PB_WG), lds, st, *K);
-        else
-            hipLaunchKernelGGL((pb_fpage_kernel<42, false>), g, dim3(PB_WG), lds, st, *K);
-    }
-    else if (K->vl)
+    if (K->vl)
     {
         const uint32_t grid = (uint32_t)((K->n_frames + K->vl_wgf - 1) / K->vl_wgf);
         const size_t lds = PB_VL_LDS(K->vl_wgf, K->hl == 54 ? 5 : 4, K->vl_nl48, K->vl_nlines) + K->lds_pad;

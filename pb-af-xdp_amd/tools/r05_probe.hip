@@ -583,33 +583,6 @@ int pr_build(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_fra
     return pr_time_launches(ctx, reps, ms, [&] { return pbk_launch_build(&K, ctx->stream); });
 }
 
-// pb_fpage_kernel at ppw pages per wave, page order ord, capped at per_cu workgroups per CU
-int pr_fpage(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, uint32_t ppw, int ord,
-             uint32_t per_cu, int reps, double *ms)
-{
-    HIPCHK(hipSetDevice(ctx->device));
-    pb_kargs K;
-    int rc = pr_kargs(ctx, seq, first, n, out, 256, &K);
-    if (rc != PBGPU_OK)
-        return rc;
-    PB_JOIN(ctx);
-    if (!K.fp || !K.xs_grid || ppw == 0 || ppw * K.fp_nf > 64 || K.hl != 42 || !(K.flags & PBK_L4_CSUM))
-        return PBGPU_EINVAL;
-    K.fp_ppw = ppw;
-    K.xs_np = 4 * ppw;
-    K.xs_grid = (uint32_t)(((uint64_t)K.xs_nch + 8ull * K.xs_np - 1) / (8ull * K.xs_np) * 8);
-    const size_t base = pbk_fpage_lds(&K);
-    const size_t target = per_cu ? PB_LDS_PER_CU / (per_cu + 1u) + 512u : 0;
-    const size_t lds = target > base ? target : base;
-    return pr_time_launches(ctx, reps, ms, [&]() -> hipError_t {
-        if (ord == 0)
-            hipLaunchKernelGGL((pb_fpage_kernel<42, true, 0>), dim3(K.xs_grid), dim3(PB_WG), lds, ctx->stream, K);
-        else
-            hipLaunchKernelGGL((pb_fpage_kernel<42, true, 1>), dim3(K.xs_grid), dim3(PB_WG), lds, ctx->stream, K);
-        return hipGetLastError();
-    });
-}
-
 // a product build with its workgroups per CU capped at per_cu by dynamic LDS (0: as loaded)
 int pr_build_cap(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, uint32_t per_cu,
                  int reps, double *ms, uint32_t *base_lds)
@@ -621,9 +594,7 @@ int pr_build_cap(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu
         return rc;
     PB_JOIN(ctx);
     size_t base = 0;
-    if (K.fp && K.xs_grid)
-        base = pbk_fpage_lds(&K);
-    else if (K.vl)
+    if (K.vl)
         base = PB_VL_LDS(K.vl_wgf, K.hl == 54 ? 5 : 4, K.vl_nl48, K.vl_nlines);
     else if (K.fst_g)
         base = (size_t)K.fst_nbuf * K.fst_sb + PB_FST_LDS(K.fst_wgf);

@@ -1,6 +1,7 @@
 """Round-5 A/B probe driver (lib/libpbprobe.so from tools/r05_probe.hip; tool only).
 
-python3 scripts/r05/probe.py xs|mix|place [reps]
+python3 scripts/r05/probe.py xs|xs8|xs9|xsapi|xp|mix|place|detect|wfill|capx [reps]
+(the pb_fpage_kernel modes "fpage" / "fpord" are in commit 37dc421 with the kernel)
   xs     64-B page-kernel shapes and the decomposition (full / stores only / arithmetic only /
          the 4-KiB fill) on one buffer, variants alternating; wave-local shapes checked
          byte for byte against the product launch
@@ -37,8 +38,6 @@ L.pr_fill_wave_at.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_u
                              C.POINTER(D)]
 L.pr_build_cap.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint32, C.c_int,
                           C.POINTER(D), C.POINTER(C.c_uint32)]
-L.pr_fpage.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint32, C.c_int, C.c_uint32,
-                      C.c_int, C.POINTER(D)]
 L.pr_xp.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_int, C.POINTER(D)]
 
 
@@ -253,72 +252,6 @@ elif what == "xsapi":
             emit(row)
     p, b = ctx.counters(1)
     emit({"counters_frames": int(p[0]), "counters_bytes": int(b[0])})
-    for fb in bufs:
-        fb.free()
-
-elif what == "fpage":
-    # the 1500-B page kernel at several occupancy caps beside pb_fstage_kernel, on NBUF large buffers
-    n = 1 << 25
-    nbuf = int(os.environ.get("NBUF", "4"))
-    ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
-    os.environ["PBGPU_KERNEL"] = "fstage"
-    ctx.load_sequence(2, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
-    del os.environ["PBGPU_KERNEL"]
-    ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
-    f0, b0 = ctx.build_size(0, n)
-    f1, b1 = ctx.build_size(1, n)
-    bufs = [ctx.alloc_frames(max(f0, f1), max(b0, b1)) for _ in range(nbuf)]
-    ref = ctx.alloc_frames(f1, b1)
-    ms = D()
-    base = C.c_uint32()
-    emit({"kernels": [ctx.kernel_name(1), ctx.kernel_name(2)]})
-    # parity at size: page kernel vs pb_fstage_kernel
-    ok(L.pr_build(ctx.h, 2, 7, n, ref.ptr, 1, C.byref(ms)), "ref")
-    ok(L.pr_build(ctx.h, 1, 7, n, bufs[0].ptr, 1, C.byref(ms)), "fpage")
-    bad = C.c_uint64()
-    ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(bufs[0])), C.c_void_p(data_ptr(ref)), n * 1500, C.byref(bad)), "cmp")
-    emit({"check": "fpage vs fstage 2^25 x 1500 B", "bad_dwords": bad.value})
-    ref.free()
-    ramp(lambda: L.pr_build(ctx.h, 1, 0, n, bufs[0].ptr, 4, C.byref(ms)))
-    for rnd in range(REPS):
-        for i, fb in enumerate(bufs):
-            row = {"round": rnd, "buf": i}
-            ok(L.pr_build(ctx.h, 0, 0, n, fb.ptr, 4, C.byref(ms)), "c3")
-            row["c3 vline"] = round(ms.value, 4)
-            ok(L.pr_build(ctx.h, 2, 0, n, fb.ptr, 4, C.byref(ms)), "fstage")
-            row["1500 fstage"] = round(ms.value, 4)
-            for cap in (0, 5, 4, 3, 2):
-                ok(L.pr_build_cap(ctx.h, 1, 0, n, fb.ptr, cap, 4, C.byref(ms), C.byref(base)), "fpage")
-                row[f"1500 fpage cap{cap}"] = round(ms.value, 4)
-            row["fpage base_lds"] = base.value
-            emit(row)
-    for fb in bufs:
-        fb.free()
-
-elif what == "fpord":
-    # pb_fpage_kernel: pages per wave x page order x occupancy, beside pb_fstage_kernel
-    n = 1 << 25
-    nbuf = int(os.environ.get("NBUF", "3"))
-    ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
-    os.environ["PBGPU_KERNEL"] = "fstage"
-    ctx.load_sequence(2, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
-    del os.environ["PBGPU_KERNEL"]
-    f1, b1 = ctx.build_size(1, n)
-    bufs = [ctx.alloc_frames(f1, b1) for _ in range(nbuf)]
-    ms = D()
-    V = [(p_, o_, c_) for p_ in (1, 2, 4, 8, 16) for o_ in (0, 1) for c_ in (0, 3)]
-    ramp(lambda: L.pr_build(ctx.h, 2, 0, n, bufs[0].ptr, 4, C.byref(ms)))
-    for rnd in range(REPS):
-        for i, fb in enumerate(bufs):
-            row = {"round": rnd, "buf": i}
-            ok(L.pr_build(ctx.h, 2, 0, n, fb.ptr, 4, C.byref(ms)), "fstage")
-            row["fstage"] = round(ms.value, 4)
-            for p_, o_, c_ in V:
-                if p_ == 1 and o_ == 1:
-                    continue
-                ok(L.pr_fpage(ctx.h, 1, 0, n, fb.ptr, p_, o_, c_, 4, C.byref(ms)), f"fpage {p_} {o_} {c_}")
-                row[f"ppw{p_} ord{o_} cap{c_}"] = round(ms.value, 4)
-            emit(row)
     for fb in bufs:
         fb.free()
 

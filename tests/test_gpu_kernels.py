@@ -65,8 +65,7 @@ SHAPES = [
 
 # pb_fstage_kernel shapes (fixed lengths > 128 B, multiple of 4, random payload)
 FST_SHAPES = [
-    ("fpage_default", {}),  # pb_fpage_kernel: one wave per XCD-owned 4-KiB page
-    ("fst_forced", {"PBGPU_KERNEL": "fstage"}),
+    ("fst_default", {}),
     ("fst_g32", {"PBGPU_FST_G": "32"}),
     ("fst_g16_nb2", {"PBGPU_FST_G": "16", "PBGPU_FST_NBUF": "2"}),
     ("fst_g64_nb1", {"PBGPU_FST_G": "64", "PBGPU_FST_NBUF": "1"}),
@@ -113,8 +112,6 @@ def test_kernel_shape_matches_oracle(ctx, monkeypatch, shape, env, kernels, name
     kern = _check(ctx, cfg, 123456789, _iters(cfg))
     if "pb_xsmall_kernel" in kernels:  # small frames keep their page kernels under the staged overrides
         kernels = kernels + ("pb_xpage_kernel",)
-    if "pb_fstage_kernel" in kernels:  # fixed lengths > 128 B: its page form in 4-KiB aligned buffers
-        kernels = kernels + ("pb_fpage_kernel",)
     assert kern.startswith(kernels), kern
 
 
@@ -220,9 +217,7 @@ def test_fstage_frames(ctx, monkeypatch, shape, env, proto, flen):
         if n * flen > (8 << 20):
             continue
         kern = _check(ctx, cfg, 77 + 3 * n, n)
-        if not env:
-            assert kern.startswith("pb_fpage_kernel<"), kern
-        elif _fst_fits(env, flen):
+        if _fst_fits(env, flen):
             assert kern.startswith("pb_fstage_kernel<%s" % env.get("PBGPU_FST_G", "")), kern
 
 
@@ -238,14 +233,11 @@ def _fst_fits(env, flen):
 
 
 @pytest.mark.parametrize("flen", [132, 1500, 1508])
-@pytest.mark.parametrize("kernel", ["fpage", "fstage"])
-def test_fstage_no_l4_csum(ctx, monkeypatch, flen, kernel):
-    if kernel == "fstage":
-        monkeypatch.setenv("PBGPU_KERNEL", "fstage")
+def test_fstage_no_l4_csum(ctx, flen):
     for proto in ("udp", "tcp", "icmp"):
         cfg = _fst_cfg(proto, flen, csum=False)
         kern = _check(ctx, cfg, 5, 1027)
-        assert kern.startswith("pb_%s_kernel<" % kernel) and kern.endswith(", 0>"), kern
+        assert kern.startswith("pb_fstage_kernel<") and kern.endswith(", 0>"), kern
 
 
 def test_fstage_not_for_other_shapes(ctx, monkeypatch):
