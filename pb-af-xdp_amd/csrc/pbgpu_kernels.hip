@@ -687,10 +687,10 @@ __global__ __launch_bounds__(WGT) void pb_xsmall_kernel(pb_kargs K)
     pb_xsmall_body<NDW, PROTO, RANDOM, WGT>(K, blockIdx.x, gridDim.x, s_tile);
 }
 
-// The round-4 64-B page body, kept for pb_batch_kernel's 64-B part: all WGT lanes build, one
-// barrier, then 256 lanes per page store it (the fused launch ran it 1% faster than the wave-local
-// body, 0.5335 vs 0.5386 ms per configs[4] step, profiles/r05/ab/mix*.jsonl: that launch runs at
-// the xpage parts' occupancy).  Workgroup b owns pages ((b / 8) np + i) 8 + b % 8, i < np =
+// The workgroup-wide 64-B page body, kept for pb_batch_kernel's 64-B part: all WGT lanes build,
+// one barrier, then each wave stores one page (the fused launch ran the round-4 form of this body
+// 1% faster than the wave-local body, 0.5335 vs 0.5386 ms per configs[4] step,
+// profiles/r05/ab/mix*.jsonl: that launch runs at the xpage parts' occupancy).  Workgroup b owns pages ((b / 8) np + i) 8 + b % 8, i < np =
 // WGT / 64 (the rest, fewer than 8 np, take the tail pages in order from xs_full).
 template <int WGT>
 __device__ __forceinline__ void pb_xsmall_wg_body(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
@@ -715,11 +715,14 @@ __device__ __forceinline__ void pb_xsmall_wg_body(const pb_kargs &K, uint32_t b,
         }
     }
     __syncthreads();
-    // page i -> HBM: lane t stores chunk t % 256 of pages t / 256, t / 256 + WGT / 256, ...
+    // page i -> HBM: wave i stores page i whole, four 1-KiB store instructions (0.530 vs 0.538 ms
+    // per configs[4] step for 1 KiB of every page per wave, profiles/r05/ab/mixws.jsonl)
+    const uint32_t i = tid >> 6, lane = tid & 63u;
+    static_assert(NPG == WGT / 64, "one page per wave");
 #pragma unroll
-    for (uint32_t u = 0; u < NPG * 256 / WGT; ++u)
+    for (uint32_t u = 0; u < 4; ++u)
     {
-        const uint32_t i = u * (WGT / 256) + tid / 256u, ch = tid % 256u;
+        const uint32_t ch = u * 64 + lane;
         const uint32_t c = c0 + i * cs;
         const uint64_t o = (uint64_t)c * PB_XPG + 16 * ch;
         if (i < np && c < K.xs_nch && o < T)
@@ -837,22 +840,29 @@ __device__ __forceinline__ void pb_xpage_body(const pb_kargs &K, uint32_t b, uin
     }
     __syncthreads();
 
-    // page i -> HBM: one 16-B store per lane per page (256 lanes per page)
-    for (uint32_t i = tid / 256; i < np; i += WGT / 256)
+    // page i -> HBM: wave w stores pages w, w + WGT / 64, ... whole, four 1-KiB store
+    // instructions each (vs 1 KiB of every other page per wave: 60-B TCP SYN 0.280-0.282 vs
+    // 0.288-0.295 ms, 98-B ICMP 0.457-0.462 vs 0.462-0.466, profiles/r05/ab/xpw3.jsonl)
+    const uint32_t lane = tid & 63u;
+    for (uint32_t i = tid >> 6; i < np; i += WGT / 64)
     {
-        const uint32_t l = tid % 256;
         const uint32_t c = c0 + i * cs;
-        const uint64_t o = (uint64_t)c * PB_XPG + 16 * l;
-        if (c < K.xs_nch && o < T)
-        {
-            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[(i * PB_XREG + 128) / 16 + l];
-            if (o + 16 > T) // last chunk of the stream: zero the tail
-            {
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
+        for (uint32_t u = 0; u < 4; ++u)
+        {
+            const uint32_t l = u * 64 + lane;
+            const uint64_t o = (uint64_t)c * PB_XPG + 16 * l;
+            if (c < K.xs_nch && o < T)
+            {
+                pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[(i * PB_XREG + 128) / 16 + l];
+                if (o + 16 > T) // last chunk of the stream: zero the tail
+                {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
+                }
+                pb_st16_nt(K.out + o, v);
             }
-            pb_st16_nt(K.out + o, v);
         }
     }
     if (tid == 0)

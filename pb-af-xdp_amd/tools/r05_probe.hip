@@ -234,6 +234,255 @@ __global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pr_x
     pb_xpage_body<NDW, PROTO, RANDOM, WGT, A4>(K, blockIdx.x, gridDim.x, s_tile);
 }
 
+// pb_xpage_body's build with wave-owned page stores: after the barrier wave w stores whole pages
+// w, w + NW, ... (four 1-KiB store instructions per page) instead of 1 KiB of every other page
+template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4>
+__device__ __forceinline__ void pr_xpage_ws_body(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
+{
+    constexpr uint32_t NW = WGT / 64;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t flen = K.fixed_len;
+    const uint32_t np = K.xs_np, fpp = K.xp_fpp;
+    const uint64_t T = K.total_bytes;
+    uint32_t c0, cs;
+    if (b < K.xs_full)
+        c0 = (b >> 3) * (np * 8) + (b & 7u), cs = 8;
+    else
+        c0 = K.xs_full * np + (b - K.xs_full) * np, cs = 1;
+    const uint64_t fa0 = pb_xp_first_frame(K, c0, flen);
+    const uint32_t rem0 = (uint32_t)((uint64_t)c0 * PB_XPG - fa0 * flen);
+#pragma unroll
+    for (uint32_t pass = 0; pass < 512 / WGT; ++pass)
+    {
+        const uint32_t sl = tid + pass * WGT;
+        if (sl >= np * fpp)
+            break;
+        const uint32_t i = pb_divq(sl, K.xp_div), j = sl - __umul24(i, fpp);
+        const uint32_t c = c0 + i * cs;
+        if (c >= K.xs_nch)
+            continue;
+        const uint32_t t = rem0 + ((i * cs) << 12);
+        const uint32_t qi = pb_divq(t, K.flen);
+        const int off = (int)__umul24(j, flen) - (int)(t - __umul24(qi, flen));
+        const uint64_t f = fa0 + qi + j;
+        if (off >= (int)PB_XPG || f >= K.n_frames)
+            continue;
+        uint32_t d[NDW];
+        pb_small_frame<NDW, PROTO, RANDOM>(K, f, d);
+        if (A4)
+        {
+            uint32_t *row = s_tile + (i * PB_XREG + 128 + off) / 4;
+#pragma unroll
+            for (int t2 = 0; t2 < NDW; t2 += 2)
+            {
+                if ((uint32_t)(4 * t2 + 4) < flen)
+                    *reinterpret_cast<pb_u32x2a4 *>(row + t2) = pb_u32x2a4{d[t2], d[t2 + 1]};
+                else if ((uint32_t)(4 * t2) < flen)
+                    row[t2] = d[t2];
+            }
+        }
+        else
+            pb_small_put<NDW, false, 2>(s_tile, d, i * PB_XREG + 128 + off, flen);
+    }
+    __syncthreads();
+    for (uint32_t i = w; i < np; i += NW)
+    {
+        const uint32_t c = c0 + i * cs;
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+        {
+            const uint32_t l = u * 64 + lane;
+            const uint64_t o = (uint64_t)c * PB_XPG + 16 * l;
+            if (c < K.xs_nch && o < T)
+            {
+                pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[(i * PB_XREG + 128) / 16 + l];
+                if (o + 16 > T)
+                {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
+                }
+                pb_st16_nt(K.out + o, v);
+            }
+        }
+    }
+    if (tid == 0)
+    {
+        uint64_t by = 0;
+        for (uint32_t i = 0; i < np; ++i)
+        {
+            const uint32_t c = c0 + i * cs;
+            if (c < K.xs_nch)
+                by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
+        }
+        pb_count_at(K, b, pb_xcd_region(b, nwg), 0, by);
+    }
+}
+
+template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4>
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pr_xpage_ws(pb_kargs K)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];
+    pr_xpage_ws_body<NDW, PROTO, RANDOM, WGT, A4>(K, blockIdx.x, gridDim.x, s_tile);
+}
+
+// pb_xsmall_wg_body with wave-owned page stores (wave w stores page w whole)
+template <int WGT>
+__device__ __forceinline__ void pr_xs_wg_ws_body(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
+{
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t np = K.xs_np;
+    const uint64_t T = K.total_bytes;
+    uint32_t c0, cs;
+    if (b < K.xs_full)
+        c0 = (b >> 3) * (np * 8) + (b & 7u), cs = 8;
+    else
+        c0 = K.xs_full * np + (b - K.xs_full) * np, cs = 1;
+    const uint32_t c = c0 + w * cs;
+    {
+        const uint64_t f = ((uint64_t)c << 6) + lane;
+        if (w < np && f < K.n_frames)
+        {
+            uint32_t d[16];
+            pb_small_frame<16, 17, true>(K, f, d);
+            pb_small_put<16, true, 16>(s_tile, d, w * PB_XREG + 128 + lane * 64, 64);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+    {
+        const uint32_t ch = u * 64 + lane;
+        const uint64_t o = (uint64_t)c * PB_XPG + 16 * ch;
+        if (w < np && c < K.xs_nch && o < T)
+        {
+            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(s_tile)[pb_swz((w * PB_XREG + 128) / 16 + ch)];
+            if (o + 16 > T)
+            {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
+            }
+            pb_st16_nt(K.out + o, v);
+        }
+    }
+    if (tid == 0)
+    {
+        uint64_t by = 0;
+        for (uint32_t i = 0; i < np; ++i)
+        {
+            const uint32_t ci = c0 + i * cs;
+            if (ci < K.xs_nch)
+                by += min((uint64_t)PB_XPG, T - (uint64_t)ci * PB_XPG);
+        }
+        pb_count_at(K, b, pb_xcd_region(b, nwg), 0, by);
+    }
+}
+
+// the fused configs[4] launch with wave-owned page stores in every part (80 SGPRs)
+template <int WGT>
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pr_mix_ws(pb_batch_args A)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];
+    const uint32_t b = blockIdx.x;
+    const uint32_t o1 = (A.g[0] + 7u) & ~7u, o2 = o1 + ((A.g[1] + 7u) & ~7u);
+    if (b < o1)
+    {
+        if (b < A.g[0])
+            pr_xs_wg_ws_body<WGT>(A.K[0], b, A.g[0], s_tile);
+    }
+    else if (b < o2)
+    {
+        if (b - o1 < A.g[1])
+            pr_xpage_ws_body<16, 6, true, WGT, true>(A.K[1], b - o1, A.g[1], s_tile);
+    }
+    else if (b - o2 < A.g[2])
+        pr_xpage_ws_body<32, 1, false, WGT, false>(A.K[2], b - o2, A.g[2], s_tile);
+}
+
+// wave-local xpage: wave w of workgroup b owns KP pages c = (((b / 8) NW + w) KP + h) 8 + b % 8,
+// builds their frame slots (ceil(KP fpp / 64) passes of its 64 lanes) into its own LDS page
+// regions and stores them (four 1-KiB stores per page) after a wave barrier only.  FMAX: the
+// most slots per page the kernel is compiled for (70 at 60 B, 43 at 98 B).  32-bit first-frame
+// arithmetic (the host refuses xp_fa_hi).
+template <int NDW, int PROTO, bool RANDOM, int WGT, bool A4, int KP, int FMAX>
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pr_xpage_wave(pb_kargs K)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];
+    constexpr uint32_t NW = WGT / 64;
+    const uint32_t b = blockIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t flen = K.fixed_len, fpp = K.xp_fpp;
+    const uint64_t T = K.total_bytes;
+    const uint32_t m0 = ((b >> 3) * NW + w) * KP;
+    uint32_t *const tile = s_tile + w * KP * (PB_XREG / 4);
+#pragma unroll
+    for (uint32_t p = 0; p < (KP * FMAX + 63) / 64; ++p)
+    {
+        const uint32_t sl = lane + 64 * p;
+        const uint32_t h = KP == 1 ? 0u : pb_divq(sl, K.xp_div);
+        const uint32_t j = sl - __umul24(h, fpp);
+        if (h >= KP || j >= fpp)
+            continue;
+        const uint32_t c = (m0 + h) * 8 + (b & 7u);
+        if (c >= K.xs_nch)
+            continue;
+        const uint32_t fa = pb_xp_first_frame(K, c, flen);
+        const uint32_t rem = c * PB_XPG - fa * flen; // < flen (mod 2^32 arithmetic)
+        const int off = (int)__umul24(j, flen) - (int)rem;
+        const uint64_t f = (uint64_t)fa + j;
+        if (off >= (int)PB_XPG || f >= K.n_frames)
+            continue;
+        uint32_t d[NDW];
+        pb_small_frame<NDW, PROTO, RANDOM>(K, f, d);
+        if (A4)
+        {
+            uint32_t *row = tile + (h * PB_XREG + 128 + off) / 4;
+#pragma unroll
+            for (int t2 = 0; t2 < NDW; t2 += 2)
+            {
+                if ((uint32_t)(4 * t2 + 4) < flen)
+                    *reinterpret_cast<pb_u32x2a4 *>(row + t2) = pb_u32x2a4{d[t2], d[t2 + 1]};
+                else if ((uint32_t)(4 * t2) < flen)
+                    row[t2] = d[t2];
+            }
+        }
+        else
+            pb_small_put<NDW, false, 2>(tile, d, h * PB_XREG + 128 + off, flen);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (uint32_t u = 0; u < 4 * KP; ++u)
+    {
+        const uint32_t h = u >> 2, l = (u & 3u) * 64 + lane;
+        const uint32_t c = (m0 + h) * 8 + (b & 7u);
+        const uint64_t o = (uint64_t)c * PB_XPG + 16 * l;
+        if (c < K.xs_nch && o < T)
+        {
+            pb_u32x4 v = reinterpret_cast<const pb_u32x4 *>(tile)[(h * PB_XREG + 128) / 16 + l];
+            if (o + 16 > T)
+            {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    v[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
+            }
+            pb_st16_nt(K.out + o, v);
+        }
+    }
+    if (threadIdx.x == 0)
+    {
+        uint64_t by = 0;
+        for (uint32_t i = 0; i < NW * KP; ++i)
+        {
+            const uint32_t c = ((b >> 3) * NW * KP + i) * 8 + (b & 7u);
+            if (c < K.xs_nch)
+                by += min((uint64_t)PB_XPG, T - (uint64_t)c * PB_XPG);
+        }
+        pb_count_at(K, b, pb_xcd_region(b, gridDim.x), 0, by);
+    }
+}
+
 // ---------------------------------------------------------------- write-only fill shapes
 // persistent XCD-owned page walker: NPP pages per step (workgroup b on XCD b % 8 takes pages
 // (m NPP + p) 8 + x, m = t Wx + j)
@@ -534,6 +783,7 @@ int pr_mix(pbgpu_ctx *ctx, const uint16_t *seqs, uint64_t first, uint64_t n, pbg
             }
             return hipSuccess;
         case 6: hipLaunchKernelGGL((pr_mix_kernel<256, 1>), dim3(grid), dim3(256), lds, st, A); break;
+        case 7: hipLaunchKernelGGL((pr_mix_ws<512>), dim3(grid), dim3(512), lds, st, A); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
@@ -568,6 +818,67 @@ int pr_xp(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames
             hipLaunchKernelGGL((pr_xpage_s80<32, 1, false, 512, false>), dim3(K.xs_grid), dim3(512), l2, st, K);
         return hipGetLastError();
     };
+    return pr_time_launches(ctx, reps, ms, launch);
+}
+
+// pb_xpage_kernel sequences, page-store shapes (lds_pad: dynamic LDS per workgroup, 0 = the
+// shape's own):  0 the product launch   1 workgroup build + wave-owned page stores (512)
+//  2 wave-local 1 page per wave, 256 threads   3 2 pages, 256   4 4 pages, 256   5 4 pages, 64
+//  6 8 pages, 64   7 2 pages, 512   8 1 page, 512
+int pr_xpw(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, int variant,
+           uint32_t lds_pad, int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr_kargs(ctx, seq, first, n, out, 256, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    PB_JOIN(ctx);
+    if (!K.xs_grid || !K.xp || K.xp_wgt != 512 || K.xp_fa_hi)
+        return PBGPU_EINVAL;
+    const int kind = pbk_batch_kind(&K);
+    if ((kind != 2 || K.xp_fpp > 70) && (kind != 3 || K.xp_fpp > 43))
+        return PBGPU_EINVAL;
+    hipStream_t st = ctx->stream;
+    const uint32_t nch = K.xs_nch;
+    static const uint32_t WG[9] = {512, 512, 256, 256, 256, 64, 64, 512, 512}, KPS[9] = {0, 0, 1, 2, 4, 4, 8, 2, 1};
+    if (variant < 0 || variant > 8)
+        return PBGPU_EINVAL;
+    const uint32_t wg = WG[variant], kp = KPS[variant];
+    const dim3 g = variant < 2 ? dim3(K.xs_grid) : dim3((nch + 8 * (wg / 64) * kp - 1) / (8 * (wg / 64) * kp) * 8);
+    const size_t own = variant < 2 ? (size_t)K.xs_np * PB_XREG : (size_t)(wg / 64) * kp * PB_XREG;
+    const size_t lds = lds_pad > own ? lds_pad : own;
+#define PR_XPW(WGT, KP)                                                                                 \
+    if (kind == 2)                                                                                      \
+        hipLaunchKernelGGL((pr_xpage_wave<16, 6, true, WGT, true, KP, 70>), g, dim3(WGT), lds, st, K);  \
+    else                                                                                                \
+        hipLaunchKernelGGL((pr_xpage_wave<32, 1, false, WGT, false, KP, 43>), g, dim3(WGT), lds, st, K)
+    auto launch = [&]() -> hipError_t {
+        switch (variant)
+        {
+        case 0:
+        {
+            pb_kargs K2 = K; // (the product adds lds_pad to its own regions)
+            K2.lds_pad = (uint32_t)(lds - own);
+            return pbk_launch_build(&K2, st);
+        }
+        case 1:
+            if (kind == 2)
+                hipLaunchKernelGGL((pr_xpage_ws<16, 6, true, 512, true>), g, dim3(512), lds, st, K);
+            else
+                hipLaunchKernelGGL((pr_xpage_ws<32, 1, false, 512, false>), g, dim3(512), lds, st, K);
+            break;
+        case 2: PR_XPW(256, 1); break;
+        case 3: PR_XPW(256, 2); break;
+        case 4: PR_XPW(256, 4); break;
+        case 5: PR_XPW(64, 4); break;
+        case 6: PR_XPW(64, 8); break;
+        case 7: PR_XPW(512, 2); break;
+        case 8: PR_XPW(512, 1); break;
+        }
+        return hipGetLastError();
+    };
+#undef PR_XPW
     return pr_time_launches(ctx, reps, ms, launch);
 }
 

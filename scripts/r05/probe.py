@@ -39,6 +39,8 @@ L.pr_fill_wave_at.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_u
 L.pr_build_cap.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint32, C.c_int,
                           C.POINTER(D), C.POINTER(C.c_uint32)]
 L.pr_xp.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_int, C.POINTER(D)]
+L.pr_xpw.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_int,
+                     C.POINTER(D)]
 
 
 def ok(rc, what):
@@ -281,6 +283,40 @@ elif what == "xp":
     for fb in bufs:
         fb.free()
 
+elif what == "xpw":
+    # page-store shapes of the 60-B / 98-B page kernels (pr_xpw), each checked byte for byte
+    # against the product launch, then timed on NBUF buffers; XPW_V: "variant:lds_pad,..."
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "4"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c4_tcp_syn")), pc.SEED_BASE)
+    ctx.load_sequence(1, Sequence.from_config(pc.get("c5_icmp_echo")), pc.SEED_BASE)
+    bufs = [ctx.alloc_frames(*ctx.build_size(1, n)) for _ in range(nbuf)]
+    ms = D()
+    names = {0: "product", 1: "wg-build wave-store", 2: "wave kp1 w256", 3: "wave kp2 w256", 4: "wave kp4 w256",
+             5: "wave kp4 w64", 6: "wave kp8 w64", 7: "wave kp2 w512", 8: "wave kp1 w512"}
+    spec = os.environ.get("XPW_V", "0:0,1:0,2:0,3:0,4:0,5:0,6:0,7:0,8:0,2:25000,3:40000,4:40000")
+    V = [(int(a), int(b)) for a, b in (x.split(":") for x in spec.split(","))]
+    for seq in (0, 1):
+        nb = n * (60 if seq == 0 else 98)
+        ok(L.pr_xpw(ctx.h, seq, 5, n, bufs[1].ptr, 0, 0, 1, C.byref(ms)), "ref")
+        for v in sorted({v for v, _ in V if v}):  # same sequence, same first iteration: byte-identical
+            ok(L.pr_xpw(ctx.h, seq, 5, n, bufs[0].ptr, v, 0, 1, C.byref(ms)), names[v])
+            bad = C.c_uint64()
+            ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(bufs[0])), C.c_void_p(data_ptr(bufs[1])), nb, C.byref(bad)),
+               "cmp")
+            emit({"check": f"seq{seq} {names[v]}", "bad_dwords": bad.value})
+    ramp(lambda: L.pr_xpw(ctx.h, 0, 0, n, bufs[0].ptr, 0, 0, 8, C.byref(ms)))
+    for r in range(REPS):
+        for i, fb in enumerate(bufs):
+            row = {"rep": r, "buf": i}
+            for seq, nm in ((0, "tcp60"), (1, "icmp98")):
+                for v, pad in V:
+                    ok(L.pr_xpw(ctx.h, seq, 0, n, fb.ptr, v, pad, 20, C.byref(ms)), nm)
+                    row[f"{nm} {names[v]}" + (f" lds{pad}" if pad else "")] = round(ms.value, 5)
+            emit(row)
+    for fb in bufs:
+        fb.free()
+
 elif what == "detect":
     # can a short probe at allocation time tell a slow placement?  Region vs page fills over
     # sub-ranges of each buffer, beside the packed and 1500-B kernels' own rates; ALLOCS
@@ -327,7 +363,10 @@ elif what == "mix":
     ms = D()
     V = [("product fused 512", 0), ("mix 512 product parts", 1), ("mix 512 wave-local 64B", 2),
          ("mix 512 wave-local 64B s80", 3), ("mix 512 product parts s80", 4), ("three launches", 5),
-         ("mix 256 wave-local 64B", 6)]
+         ("mix 256 wave-local 64B", 6), ("mix 512 wave-owned stores s80", 7)]
+    if os.environ.get("MIX_V"):
+        keep = {int(x) for x in os.environ["MIX_V"].split(",")}
+        V = [(nm, v) for nm, v in V if v in keep]
     ok(L.pr_mix(ctx.h, seqs, 3, n, routs, 5, 1, C.byref(ms)), "ref")
     for name, v in V:
         ok(L.pr_mix(ctx.h, seqs, 3, n, outs, v, 1, C.byref(ms)), name)
