@@ -39,6 +39,8 @@ L.pr_fill_wave_at.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_u
 L.pr_build_cap.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint32, C.c_int,
                           C.POINTER(D), C.POINTER(C.c_uint32)]
 L.pr_xp.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_int, C.POINTER(D)]
+L.pr_fxp.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_int,
+                     C.POINTER(D)]
 L.pr_xpw.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_int,
                      C.POINTER(D)]
 
@@ -313,6 +315,43 @@ elif what == "xpw":
                 for v, pad in V:
                     ok(L.pr_xpw(ctx.h, seq, 0, n, fb.ptr, v, pad, 20, C.byref(ms)), nm)
                     row[f"{nm} {names[v]}" + (f" lds{pad}" if pad else "")] = round(ms.value, 5)
+            emit(row)
+    for fb in bufs:
+        fb.free()
+
+elif what == "fxp":
+    # page-owned 1500-B writer (pr_fxp) vs pb_fstage_kernel on NBUF 50-GB buffers alive at once;
+    # each variant checked byte for byte against the product launch first.  FXP_V "variant:lds,..."
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "4"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
+    bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(nbuf)]
+    ms = D()
+    names = {0: "fstage", 1: "fxp np4", 2: "fxp np4 nt", 3: "fxp np8", 4: "fxp np2", 5: "fxp A only",
+             6: "fxp A+B no stores", 7: "fxp B+S trivial A"}
+    spec = os.environ.get("FXP_V", "0:0,1:0,2:0,3:0,4:0,1:32000,1:40000")
+    V = [(int(a), int(b)) for a, b in (x.split(":") for x in spec.split(","))]
+    cn = int(os.environ.get("FXP_CHECK_N", str(1 << 22)))
+    for v in sorted({v for v, _ in V if 0 < v < 5}):
+        ok(L.pr_fxp(ctx.h, 0, 5, cn, bufs[1].ptr, 0, 0, 1, C.byref(ms)), "ref")
+        ok(L.pr_fxp(ctx.h, 0, 5, cn, bufs[0].ptr, v, 0, 1, C.byref(ms)), names[v])
+        bad = C.c_uint64()
+        ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(bufs[0])), C.c_void_p(data_ptr(bufs[1])), cn * 1500, C.byref(bad)),
+           "cmp")
+        emit({"check": names[v], "frames": cn, "bad_dwords": bad.value})
+        # an odd-sized build: the stream's last page is partial
+        ok(L.pr_fxp(ctx.h, 0, 7, 12345, bufs[1].ptr, 0, 0, 1, C.byref(ms)), "ref")
+        ok(L.pr_fxp(ctx.h, 0, 7, 12345, bufs[0].ptr, v, 0, 1, C.byref(ms)), names[v])
+        ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(bufs[0])), C.c_void_p(data_ptr(bufs[1])), 12345 * 1500,
+                        C.byref(bad)), "cmp")
+        emit({"check": names[v], "frames": 12345, "bad_dwords": bad.value})
+    ramp(lambda: L.pr_fxp(ctx.h, 0, 0, n, bufs[0].ptr, 0, 0, 2, C.byref(ms)))
+    for r in range(REPS):
+        for i, fb in enumerate(bufs):
+            row = {"rep": r, "buf": i}
+            for v, pad in V:
+                ok(L.pr_fxp(ctx.h, 0, 0, n, fb.ptr, v, pad, 5, C.byref(ms)), names[v])
+                row[names[v] + (f" lds{pad}" if pad else "")] = round(ms.value, 4)
             emit(row)
     for fb in bufs:
         fb.free()
