@@ -32,6 +32,8 @@ extern "C" int pbk_batch_kind(const pb_kargs *K);
 extern "C" hipError_t pbk_launch_batch(const pb_kargs *Ks, uint32_t wgt, hipStream_t st);
 extern "C" hipError_t pbk_launch_ctr_fold(const uint32_t *slots, uint64_t n, uint32_t pairs,
                                           unsigned long long *counters, hipStream_t st);
+extern "C" hipError_t pbk_launch_ctr_read(const unsigned long long *counters, uint32_t n_seq, unsigned long long *out,
+                                          hipStream_t st);
 extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *block_sums, uint32_t nblocks,
                                          uint64_t *offsets, hipStream_t st);
 extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t wgf, uint32_t *bsum, uint32_t nblk,
@@ -248,6 +250,9 @@ struct pbgpu_ctx
     uint32_t *d_orbit = nullptr; // pb_vline_kernel: LCG-orbit prefix sums (built on first use, 2 MiB)
     uint32_t orbit_tot = 0;
     unsigned long long *d_counters = nullptr; // [PB_MAX_SEQUENCES][PB_CTR_SHARDS][PB_CTR_STRIDE]
+    // the shard sums {frames, bytes} per sequence, written by pb_ctr_read into mapped pinned host
+    // memory (h_ctr_sum; d_ctr_sum its device address)
+    unsigned long long *h_ctr_sum = nullptr, *d_ctr_sum = nullptr;
     seq_slot seqs[PB_MAX_SEQUENCES];
     std::vector<timing_pair> pending;
     std::vector<timing_pair> pool;
@@ -563,7 +568,8 @@ static int join_builds(pbgpu_ctx *ctx)
     return PBGPU_OK;
 }
 
-static void slot_counts(const pbgpu_ctx *ctx, const unsigned long long *h, int i, uint64_t *p, uint64_t *b);
+static void slot_counts(const pbgpu_ctx *ctx, const unsigned long long *sum, int i, uint64_t *p, uint64_t *b);
+static int read_counter_sums(pbgpu_ctx *ctx, int first, int n_seq);
 
 // Launches that touch a sequence's count ring (its builds and folds) run in order, whatever
 // stream each is issued on: the next one waits for the previous one's stream.
@@ -654,7 +660,10 @@ int pbgpu_open(int device, pbgpu_ctx **out)
     }
     if (upload(&ctx->d_jump, jt.data(), jt.size()) != PBGPU_OK || upload(&ctx->d_lcg48, l48.data(), l48.size()) != PBGPU_OK ||
         hipMalloc((void **)&ctx->d_counters, PB_CTR_BYTES) != hipSuccess ||
-        hipMemset(ctx->d_counters, 0, PB_CTR_BYTES) != hipSuccess)
+        hipMemset(ctx->d_counters, 0, PB_CTR_BYTES) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->h_ctr_sum, 2 * sizeof(unsigned long long) * PB_MAX_SEQUENCES,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&ctx->d_ctr_sum, ctx->h_ctr_sum, 0) != hipSuccess)
     {
         pbgpu_close(ctx);
         return PBGPU_EIO;
@@ -703,6 +712,8 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipFree(ctx->d_orbit);
     if (ctx->d_counters)
         (void)hipFree(ctx->d_counters);
+    if (ctx->h_ctr_sum)
+        (void)hipHostFree(ctx->h_ctr_sum);
     if (ctx->h_stage)
         (void)hipHostFree(ctx->h_stage);
     if (ctx->d_lens)
@@ -740,14 +751,14 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     seq_slot &S = ctx->seqs[seq_idx];
     if (S.loaded) // the slot's counts so far (their frames follow the old sequence's length)
     {
-        std::vector<unsigned long long> h(PB_CTR_WORDS);
-        unsigned long long *dc = ctx->d_counters + PB_CTR_WORDS * seq_idx;
-        HIPCHK(hipMemcpy(h.data(), dc, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost));
+        const int rrc = read_counter_sums(ctx, seq_idx, 1);
+        if (rrc != PBGPU_OK)
+            return rrc;
         uint64_t p = 0, b = 0;
-        slot_counts(ctx, h.data(), seq_idx, &p, &b);
+        slot_counts(ctx, ctx->h_ctr_sum, seq_idx, &p, &b);
         ctx->ctr_base[seq_idx][0] = p;
         ctx->ctr_base[seq_idx][1] = b;
-        HIPCHK(hipMemset(dc, 0, h.size() * sizeof(h[0])));
+        HIPCHK(hipMemset(ctx->d_counters + PB_CTR_WORDS * seq_idx, 0, PB_CTR_WORDS * sizeof(unsigned long long)));
     }
     {
         // the count ring (empty now) stays with the slot
@@ -2161,19 +2172,28 @@ int pbgpu_copy_to_umem(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, uint32
 // A slot's device counters: the shards' sums; fixed-length kernels add only the bytes they
 // stored (one atomic per workgroup: each is a memory-side transaction, 0.4-1% of a small-frame
 // launch's traffic as two), so their frames are bytes / length.
-static void slot_counts(const pbgpu_ctx *ctx, const unsigned long long *h, int i, uint64_t *p, uint64_t *b)
+// sum: slot i's shard sums {frames, bytes} (read_counter_sums)
+static void slot_counts(const pbgpu_ctx *ctx, const unsigned long long *sum, int i, uint64_t *p, uint64_t *b)
 {
-    uint64_t pp = 0, bb = 0;
-    for (size_t k = 0; k < PB_CTR_SHARDS; ++k)
-    {
-        pp += h[k * PB_CTR_STRIDE + 0];
-        bb += h[k * PB_CTR_STRIDE + 1];
-    }
+    uint64_t pp = sum[0], bb = sum[1];
     const seq_slot &S = ctx->seqs[i];
     if (S.loaded && S.K.fixed_len)
         pp = bb / S.K.fixed_len;
     *p = pp + ctx->ctr_base[i][0];
     *b = bb + ctx->ctr_base[i][1];
+}
+
+// Slots [first, first + n_seq)'s shard sums into ctx->h_ctr_sum[2 (i - first) ..], by a kernel
+// writing the mapped host buffer (on ctx->stream, after everything issued there), then a stream
+// synchronisation.  A pageable hipMemcpy of the shards instead (8 KiB per slot) cost 8-16 ms on
+// its first use for three slots, an idle gap before bench.py's timed configs[4] steps that cost
+// their first 25 launches up to 30% (profiles/r05/ab/gap.log, profiles/r05/prof/cfg/trace_c5_mix*)
+static int read_counter_sums(pbgpu_ctx *ctx, int first, int n_seq)
+{
+    HIPCHK(pbk_launch_ctr_read(ctx->d_counters + PB_CTR_WORDS * (size_t)first, (uint32_t)n_seq,
+                               ctx->d_ctr_sum, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PBGPU_OK;
 }
 
 int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)
@@ -2191,13 +2211,13 @@ int pbgpu_counters(pbgpu_ctx *ctx, uint64_t *pckts, uint64_t *bytes, int n_seq)
         if (frc != PBGPU_OK)
             return frc;
     }
-    std::vector<unsigned long long> h(PB_CTR_WORDS * (size_t)n_seq);
-    HIPCHK(hipMemcpyAsync(h.data(), ctx->d_counters, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    const int rrc = read_counter_sums(ctx, 0, n_seq);
+    if (rrc != PBGPU_OK)
+        return rrc;
     for (int i = 0; i < n_seq; ++i)
     {
         uint64_t p = 0, b = 0;
-        slot_counts(ctx, h.data() + PB_CTR_WORDS * i, i, &p, &b);
+        slot_counts(ctx, ctx->h_ctr_sum + 2 * i, i, &p, &b);
         if (pckts)
             pckts[i] = p;
         if (bytes)

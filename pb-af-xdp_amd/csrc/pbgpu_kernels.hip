@@ -360,6 +360,30 @@ __global__ __launch_bounds__(256) void pb_ctr_fold(const uint32_t *slots, uint64
     }
 }
 
+// The counters' shard sums {frames, bytes} of sequences [0, n_seq), written straight into mapped
+// pinned host memory (out: its device address, 2 n_seq words): pbgpu_counters' readback without a
+// DMA copy (a pageable 24-KiB hipMemcpy of three sequences' shards took 8-16 ms the first time in a
+// process, an idle gap right before bench.py's timed steps; profiles/r05/ab/gap.log)
+__global__ __launch_bounds__(64) void pb_ctr_read(const unsigned long long *counters, uint32_t n_seq,
+                                                  unsigned long long *out)
+{
+    for (uint32_t w = threadIdx.x; w < 2 * n_seq; w += 64)
+    {
+        const unsigned long long *c = counters + (size_t)(w >> 1) * PB_CTR_SHARDS * PB_CTR_STRIDE + (w & 1u);
+        unsigned long long t = 0;
+        for (uint32_t k = 0; k < PB_CTR_SHARDS; ++k)
+            t += c[(size_t)k * PB_CTR_STRIDE];
+        out[w] = t;
+    }
+}
+
+extern "C" hipError_t pbk_launch_ctr_read(const unsigned long long *counters, uint32_t n_seq, unsigned long long *out,
+                                          hipStream_t st)
+{
+    hipLaunchKernelGGL(pb_ctr_read, dim3(1), dim3(64), 0, st, counters, n_seq, out);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t pbk_launch_ctr_fold(const uint32_t *slots, uint64_t n, uint32_t pairs,
                                           unsigned long long *counters, hipStream_t st)
 {
@@ -526,11 +550,16 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
         const uint32_t nw = (flen - 2u) >> 2;
         const uint32_t sh = B & 2u; // 2: starts at byte 2 of a dword, the half dword comes first
         uint16_t *const half = reinterpret_cast<uint16_t *>(s_tile) + ((sh ? B : B + flen - 2u) >> 1);
-        *half = (uint16_t)(sh ? d[0] : (d[nw] & 0xFFFFu));
         uint32_t *const row = s_tile + ((B + sh) >> 2);
+        uint32_t last = 0; // d[nw], picked at the pair whose range holds nw (uniform): d[nw] with
+                           // nw known only at run time compiled to a compare + select per dword
 #pragma unroll
         for (int u = 0; u < NDW; u += 2)
         {
+            if ((uint32_t)u == nw)
+                last = d[u];
+            else if ((uint32_t)u + 1u == nw && u + 1 < NDW)
+                last = d[u + 1];
             if ((uint32_t)u < nw)
             {
                 // v_alignbyte by sh bytes: the frame's dwords as they are (sh = 0) or moved down two
@@ -545,6 +574,7 @@ __device__ __forceinline__ void pb_small_put(uint32_t *s_tile, const uint32_t (&
                     row[u] = v0;
             }
         }
+        *half = (uint16_t)(sh ? d[0] : (last & 0xFFFFu));
     }
     else
     {
@@ -2809,7 +2839,7 @@ static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
             else
                 hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, false, PB_WG>), g, dim3(PB_WG), lds, st, *K);
         }
-        else // 2 mod 4: only under PBGPU_XP_FORCE (experiments)
+        else // 2 mod 4: static-payload frames (98-B ICMP); any even length under PBGPU_XP_FORCE
         {
             if (K->pl0.random && w512)
                 hipLaunchKernelGGL((pb_xpage_kernel<NDW, PROTO, true, 512, false>), g, dim3(512), lds, st, *K);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A round's profile evidence on the current tree (ROUND=r04 by default):
+# A round's profile evidence on the current tree (ROUND=r05 by default):
 #   1. the GPU suite and smoke;
 #   2. rocprofv3 --kernel-trace --stats of the default bench command (trace summary of its timed window);
 #   3. separate --pmc passes per BASELINE config (WRITE_SIZE / FETCH_SIZE / SQ issue / LDS) ->
@@ -8,10 +8,10 @@
 # Output: gpurun_out/prof_$ROUND/ (copied to profiles/$ROUND/prof/ afterwards).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-ROUND=${ROUND:-r04}
+ROUND=${ROUND:-r05}
 OUT=gpurun_out/prof_$ROUND
 PMC=profiles/pmc_$ROUND.json
-rm -rf $OUT; mkdir -p $OUT/cfg
+[ -z "$KEEP_OUT" ] && rm -rf $OUT; mkdir -p $OUT/cfg
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
   rc=$?
@@ -20,10 +20,10 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || exit 1
   echo "tests + smoke ok"
 fi
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench_trace -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-seconds 2 > $OUT/bench_trace.log 2>&1 || { echo TRACE_FAIL; tail -5 $OUT/bench_trace.log; exit 1; }
+[ -z "$SKIP_TRACE" ] && { timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench_trace -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-seconds 2 > $OUT/bench_trace.log 2>&1 || { echo TRACE_FAIL; tail -5 $OUT/bench_trace.log; exit 1; }
 grep '^{"metric"' $OUT/bench_trace.log > $OUT/bench_under_trace.json
 python3 scripts/trace_summary.py $OUT/bench_trace/run_kernel_trace.csv $OUT/kernel_trace_summary.json
-echo "trace done"
+echo "trace done"; }
 if [ -z "$SKIP_PMC" ]; then
   for cfg in c2_udp_64 c2_udp_1500 c3_udp_var c4_tcp_syn c5_icmp_echo c5_mix; do
     P=33554432; [ $cfg = c5_mix ] && P=16777216
@@ -37,6 +37,7 @@ if [ -z "$SKIP_PMC" ]; then
   python3 scripts/pmc_collect.py $OUT
   cp $OUT/pmc_summary.json $PMC
 fi
+[ -n "$SKIP_CFG" ] && exit 0
 for cfg in c2_udp_64 c2_udp_1500 c3_udp_var c4_tcp_syn c5_icmp_echo c5_mix; do
   V=--no-variants; [ $cfg = c3_udp_var ] && V=
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/cfg/trace_$cfg -o run -- python3 bench.py --steps 50 --warmup 5 $V --cpu-seconds 0 --config $cfg --pmc $PMC > $OUT/cfg/$cfg.log 2>&1 || { echo "CFG_FAIL $cfg"; tail -5 $OUT/cfg/$cfg.log; exit 1; }

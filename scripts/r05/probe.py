@@ -41,6 +41,10 @@ L.pr_build_cap.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_v
 L.pr_xp.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_int, C.POINTER(D)]
 L.pr_fxp.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_int,
                      C.POINTER(D)]
+L.pr_frames_vmm.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p),
+                           C.POINTER(C.c_uint64)]
+L.pr_frames_vmm_free.argtypes = [C.c_void_p, C.c_void_p]
+L.pr_frames_vmm_free.restype = None
 L.pr_xpw.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_int,
                      C.POINTER(D)]
 
@@ -355,6 +359,72 @@ elif what == "fxp":
             emit(row)
     for fb in bufs:
         fb.free()
+
+elif what == "vmm":
+    # does the VA -> physical chunk order decide the region kernels' slow placement?  Frame
+    # buffers from hipMalloc vs physical chunks (hipMemCreate) mapped in creation order or
+    # shuffled; per allocation kind NBUF buffers, configs[2] and 1500-B builds plus two fills
+    import pbgpu as pg
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "2"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
+    ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
+    f0, b0 = ctx.build_size(0, n)
+    f1, b1 = ctx.build_size(1, n)
+    nf, nb = max(f0, f1), max(b0, b1)
+    MB = 1 << 20
+    kinds = [("malloc", 0, 0), ("vmm 2M in order", 2 * MB, 0), ("vmm 2M shuffled", 2 * MB, 7),
+             ("vmm 64M in order", 64 * MB, 0), ("vmm 64M shuffled", 64 * MB, 7), ("vmm 1G shuffled", 1024 * MB, 7)]
+    if os.environ.get("VMM_K"):
+        keep = {int(x) for x in os.environ["VMM_K"].split(",")}
+        kinds = [k for i, k in enumerate(kinds) if i in keep]
+    ms = D()
+    ref = None
+    for alloc in range(int(os.environ.get("ALLOCS", "2"))):
+        for label, chunk, shuf in kinds:
+            bufs = []
+            t0 = time.perf_counter()
+            for i in range(nbuf):
+                if chunk == 0:
+                    bufs.append(("m", ctx.alloc_frames(nf, nb)))
+                else:
+                    p = C.c_void_p()
+                    g = C.c_uint64()
+                    ok(L.pr_frames_vmm(ctx.h, nf, nb, chunk, shuf + 1000 * alloc + i if shuf else 0, C.byref(p),
+                                       C.byref(g)), label)
+                    bufs.append(("v", p))
+            t_alloc = time.perf_counter() - t0
+            for i, (kind, b) in enumerate(bufs):
+                ptr = b.ptr if kind == "m" else b
+                fr = C.cast(ptr, C.POINTER(pg.Frames)).contents
+                if alloc == 0 and i == 0 and chunk == 0:
+                    ramp(lambda: L.pr_build(ctx.h, 1, 0, n, ptr, 4, C.byref(ms)))
+                row = {"alloc": alloc, "kind": label, "buf": i, "alloc_s": round(t_alloc, 2), "addr": hex(fr.data or 0)}
+                ok(L.pr_build(ctx.h, 0, 0, n, ptr, 5, C.byref(ms)), "c3")
+                row["c3_ms"] = round(ms.value, 4)
+                ok(L.pr_build(ctx.h, 1, 0, n, ptr, 5, C.byref(ms)), "1500")
+                row["c2_1500_ms"] = round(ms.value, 4)
+                for sh, nm in ((1, "reg208 TB/s"), (0, "4KiB/wg TB/s")):
+                    ok(L.pr_fill(ctx.h, C.c_void_p(fr.data), n * 1500, sh, 2048, 5, C.byref(ms)), nm)
+                    row[nm] = round(n * 1500 / (ms.value * 1e-3) / 1e12, 3)
+                emit(row)
+            # parity of a build into a chunk-mapped buffer against a hipMalloc'ed one
+            if alloc == 0 and chunk and shuf:
+                if ref is None:
+                    ref = ctx.alloc_frames(nf, nb)
+                ok(L.pr_build(ctx.h, 1, 3, 1 << 22, ref.ptr, 1, C.byref(ms)), "ref")
+                ok(L.pr_build(ctx.h, 1, 3, 1 << 22, bufs[0][1], 1, C.byref(ms)), "vmm")
+                bad = C.c_uint64()
+                dv = C.cast(bufs[0][1], C.POINTER(pg.Frames)).contents.data
+                ok(L.pr_compare(ctx.h, C.c_void_p(dv), C.c_void_p(ref.f.data), (1 << 22) * 1500, C.byref(bad)), "cmp")
+                emit({"check": label, "bad_dwords": bad.value})
+                ref.free()
+                ref = None
+            for kind, b in bufs:
+                if kind == "m":
+                    b.free()
+                else:
+                    L.pr_frames_vmm_free(ctx.h, b)
 
 elif what == "detect":
     # can a short probe at allocation time tell a slow placement?  Region vs page fills over
