@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <unordered_map>
 #include <new>
 #include <deque>
 #include <vector>
@@ -110,6 +111,8 @@ struct pb_opts
     bool seq_streams = true; // PBGPU_SEQ_STREAMS=0: span-mode builds all on the context's stream
     bool land_spin = true;   // PBGPU_LAND_SPIN=0: blocking landing waits
     bool umem_dma = false;   // PBGPU_UMEM_DMA=1: land through DMA copies, not the mapped scatter
+    bool alloc_vmm = true;   // PBGPU_ALLOC=malloc: frame buffers from hipMalloc (fb_alloc)
+    uint32_t alloc_chunk_mb = 64; // PBGPU_ALLOC_CHUNK_MB: fb_alloc's physical chunk
 };
 
 uint32_t opt_u32(const char *name)
@@ -161,6 +164,9 @@ pb_opts read_opts()
     o.seq_streams = !opt_is("PBGPU_SEQ_STREAMS", "0");
     o.land_spin = !opt_is("PBGPU_LAND_SPIN", "0");
     o.umem_dma = getenv("PBGPU_UMEM_DMA") != NULL;
+    o.alloc_vmm = !opt_is("PBGPU_ALLOC", "malloc");
+    if (opt_u32("PBGPU_ALLOC_CHUNK_MB"))
+        o.alloc_chunk_mb = opt_u32("PBGPU_ALLOC_CHUNK_MB");
     return o;
 }
 
@@ -1338,6 +1344,111 @@ int pbgpu_build_size(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t n_iter, uint64_t
     return PBGPU_OK;
 }
 
+// Device memory of frame buffers.  A buffer of >= PB_VMM_MIN bytes is built from physical chunks
+// (hipMemCreate, alloc_chunk_mb each) mapped in creation order into one reserved VA range,
+// instead of one hipMalloc: the region kernels' slow mode follows the buffer's
+// physical placement, and hipMalloc'ed 50-GB buffers drew it on four of five allocations in one
+// process (pb_fstage_kernel 7.28-7.34 ms, pb_vline_kernel 4.89-4.96) where chunk-mapped ones did
+// on none (7.04-7.15 / 4.22-4.71; profiles/r05/ab/vmm*.jsonl).  Falls back to hipMalloc when the
+// virtual-memory calls fail.  The blocks are kept in a process-wide table: fb_free needs no context.
+#define PB_VMM_MIN (64ull << 20)
+
+namespace
+{
+struct vmm_block
+{
+    size_t bytes;
+    std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks; // handle, size
+};
+std::mutex g_vmm_mu;
+std::unordered_map<void *, vmm_block> g_vmm;
+
+void vmm_release(void *va, vmm_block &B)
+{
+    size_t off = 0;
+    for (auto &c : B.chunks)
+    {
+        (void)hipMemUnmap((char *)va + off, c.second);
+        (void)hipMemRelease(c.first);
+        off += c.second;
+    }
+    (void)hipMemAddressFree(va, B.bytes);
+}
+} // namespace
+
+static hipError_t fb_alloc(const pbgpu_ctx *ctx, void **p, size_t bytes)
+{
+    *p = nullptr;
+    const size_t chunk = (size_t)ctx->opt.alloc_chunk_mb << 20;
+    if (!ctx->opt.alloc_vmm || bytes < PB_VMM_MIN || chunk == 0)
+        return hipMalloc(p, bytes);
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = ctx->device;
+    size_t gran = 0;
+    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess || gran == 0 ||
+        chunk % gran)
+        return hipMalloc(p, bytes);
+    vmm_block B;
+    B.bytes = (bytes + gran - 1) / gran * gran;
+    void *va = nullptr;
+    if (hipMemAddressReserve(&va, B.bytes, chunk, nullptr, 0) != hipSuccess)
+        return hipMalloc(p, bytes);
+    bool ok = true;
+    for (size_t off = 0; off < B.bytes && ok; off += chunk)
+    {
+        const size_t sz = B.bytes - off < chunk ? B.bytes - off : chunk;
+        hipMemGenericAllocationHandle_t h;
+        if (hipMemCreate(&h, sz, &prop, 0) != hipSuccess)
+        {
+            ok = false;
+            break;
+        }
+        if (hipMemMap((char *)va + off, sz, 0, h, 0) != hipSuccess)
+        {
+            (void)hipMemRelease(h);
+            ok = false;
+            break;
+        }
+        B.chunks.push_back({h, sz});
+    }
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    if (ok && hipMemSetAccess(va, B.bytes, &acc, 1) != hipSuccess)
+        ok = false;
+    if (!ok)
+    {
+        vmm_release(va, B); // the chunks mapped so far, then the reservation
+        (void)hipGetLastError();
+        return hipMalloc(p, bytes);
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_vmm_mu);
+        g_vmm.emplace(va, std::move(B));
+    }
+    *p = va;
+    return hipSuccess;
+}
+
+static void fb_free(void *p)
+{
+    if (p == nullptr)
+        return;
+    {
+        std::lock_guard<std::mutex> lk(g_vmm_mu);
+        auto it = g_vmm.find(p);
+        if (it != g_vmm.end())
+        {
+            vmm_release(p, it->second);
+            g_vmm.erase(it);
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+
 int pbgpu_frames_alloc(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capacity_bytes, pbgpu_frames **out)
 {
     if (ctx == NULL || out == NULL)
@@ -1348,8 +1459,8 @@ int pbgpu_frames_alloc(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capaci
         return PBGPU_ENOMEM;
     capacity_bytes = (capacity_bytes + 15) & ~15ull;
     // +64 B: word-granular readers (UMEM scatter) may touch a few bytes past the last frame
-    if (hipMalloc((void **)&f->data, capacity_bytes + 64) != hipSuccess ||
-        hipMalloc((void **)&f->offsets, (capacity_frames + 1) * sizeof(uint64_t)) != hipSuccess ||
+    if (fb_alloc(ctx, (void **)&f->data, capacity_bytes + 64) != hipSuccess ||
+        fb_alloc(ctx, (void **)&f->offsets, (capacity_frames + 1) * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc((void **)&f->scan_tmp, scan_tmp_bytes(capacity_frames)) != hipSuccess)
     {
         pbgpu_frames_free(ctx, f);
@@ -1382,7 +1493,7 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
         if (fe->moved)
             (void)hipEventDestroy(fe->moved);
         if (fe->d_off32)
-            (void)hipFree(fe->d_off32);
+            fb_free(fe->d_off32);
         if (fe->d_rstart)
             (void)hipFree(fe->d_rstart);
         if (fe->landed)
@@ -1390,9 +1501,9 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
         delete fe;
     }
     if (f->data)
-        (void)hipFree(f->data);
+        fb_free(f->data);
     if (f->offsets)
-        (void)hipFree(f->offsets);
+        fb_free(f->offsets);
     if (f->scan_tmp)
         (void)hipFree(f->scan_tmp);
     free(f);
@@ -1575,7 +1686,7 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
                 // (each checked on its own: a failed second allocation must not leave the pair
                 // half set for the next build to launch with a null region-start array)
                 if (fe->d_off32 == nullptr)
-                    HIPCHK(hipMalloc((void **)&fe->d_off32, (out->capacity_frames + 1) * sizeof(uint32_t)));
+                    HIPCHK(fb_alloc(ctx, (void **)&fe->d_off32, (out->capacity_frames + 1) * sizeof(uint32_t)));
                 if (fe->d_rstart == nullptr)
                     HIPCHK(hipMalloc((void **)&fe->d_rstart, (out->capacity_frames / 32 + 2) * sizeof(unsigned long long)));
                 K.offsets32 = fe->d_off32;

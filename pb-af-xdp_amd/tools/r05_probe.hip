@@ -1143,6 +1143,134 @@ int pr_fxp(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frame
     return pr_time_launches(ctx, reps, ms, launch);
 }
 
+// A frame buffer whose bytes are physical chunks of `chunk` bytes created one by one
+// (hipMemCreate) and mapped into one reserved VA range in a chosen order: shuffle 0 in creation
+// order, else a Fisher-Yates permutation seeded by `shuffle`.  The placement study: does the VA ->
+// physical chunk order decide the region kernels' slow mode?  Frees with pr_frames_vmm_free.
+struct pr_vmm
+{
+    pbgpu_frames *f;
+    void *va, *ova; // frame bytes; offsets (null: the library's hipMalloc)
+    size_t bytes, chunk, obytes;
+    std::vector<hipMemGenericAllocationHandle_t> h, oh;
+};
+
+// reserve `bytes` (a multiple of chunk) and map physical chunks created in order into it
+static int pr_vmm_map(size_t bytes, size_t chunk, uint64_t shuffle, const hipMemAllocationProp &prop, void **va,
+                      std::vector<hipMemGenericAllocationHandle_t> &h)
+{
+    const size_t n = bytes / chunk;
+    HIPCHK(hipMemAddressReserve(va, bytes, chunk, nullptr, 0));
+    std::vector<size_t> perm(n);
+    for (size_t i = 0; i < n; ++i)
+        perm[i] = i;
+    if (shuffle)
+    {
+        uint64_t x = shuffle;
+        for (size_t i = n - 1; i > 0; --i)
+        {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            const size_t j = (size_t)((x >> 33) % (i + 1));
+            std::swap(perm[i], perm[j]);
+        }
+    }
+    h.resize(n);
+    for (size_t i = 0; i < n; ++i)
+    {
+        HIPCHK(hipMemCreate(&h[i], chunk, &prop, 0));
+        HIPCHK(hipMemMap((char *)*va + perm[i] * chunk, chunk, 0, h[i], 0));
+    }
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    HIPCHK(hipMemSetAccess(*va, bytes, &acc, 1));
+    return PBGPU_OK;
+}
+
+static void pr_vmm_unmap(void *va, size_t chunk, std::vector<hipMemGenericAllocationHandle_t> &h)
+{
+    for (size_t c = 0; c < h.size(); ++c)
+        (void)hipMemUnmap((char *)va + c * chunk, chunk);
+    for (auto x : h)
+        (void)hipMemRelease(x);
+    (void)hipMemAddressFree(va, h.size() * chunk);
+    h.clear();
+}
+static std::vector<pr_vmm *> &pr_vmm_live()
+{
+    static std::vector<pr_vmm *> v;
+    return v;
+}
+
+// flags bit 0: the offsets array from chunks too
+int pr_frames_vmm(pbgpu_ctx *ctx, uint64_t capacity_frames, uint64_t capacity_bytes, uint64_t chunk, uint64_t shuffle,
+                  pbgpu_frames **out, uint64_t *gran_out, uint32_t flags)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = ctx->device;
+    size_t gran = 0;
+    HIPCHK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
+    if (gran_out)
+        *gran_out = gran;
+    if (chunk == 0 || chunk % gran)
+        return PBGPU_EINVAL;
+    pbgpu_frames *f = nullptr;
+    int rc = pbgpu_frames_alloc(ctx, capacity_frames, 16, &f);
+    if (rc != PBGPU_OK)
+        return rc;
+    HIPCHK(hipFree(f->data));
+    f->data = nullptr;
+    pr_vmm *V = new pr_vmm;
+    V->f = f;
+    V->chunk = chunk;
+    V->ova = nullptr;
+    const size_t need = ((capacity_bytes + 15) & ~15ull) + 64;
+    V->bytes = (need + chunk - 1) / chunk * chunk;
+    if ((rc = pr_vmm_map(V->bytes, chunk, shuffle, prop, &V->va, V->h)) != PBGPU_OK)
+        return rc;
+    f->data = (uint8_t *)V->va;
+    f->capacity_bytes = (capacity_bytes + 15) & ~15ull;
+    if (flags & 1u)
+    {
+        HIPCHK(hipFree(f->offsets));
+        f->offsets = nullptr;
+        const size_t ob = (capacity_frames + 1) * sizeof(uint64_t);
+        const size_t oc = 2u << 20; // 2-MiB chunks
+        V->obytes = (ob + oc - 1) / oc * oc;
+        if ((rc = pr_vmm_map(V->obytes, oc, 0, prop, &V->ova, V->oh)) != PBGPU_OK)
+            return rc;
+        f->offsets = (uint64_t *)V->ova;
+    }
+    pr_vmm_live().push_back(V);
+    *out = f;
+    return PBGPU_OK;
+}
+
+void pr_frames_vmm_free(pbgpu_ctx *ctx, pbgpu_frames *f)
+{
+    (void)hipDeviceSynchronize();
+    auto &L = pr_vmm_live();
+    for (size_t i = 0; i < L.size(); ++i)
+        if (L[i]->f == f)
+        {
+            pr_vmm *V = L[i];
+            pr_vmm_unmap(V->va, V->chunk, V->h);
+            f->data = nullptr;
+            if (V->ova)
+            {
+                pr_vmm_unmap(V->ova, 2u << 20, V->oh);
+                f->offsets = nullptr;
+            }
+            L.erase(L.begin() + (long)i);
+            delete V;
+            break;
+        }
+    pbgpu_frames_free(ctx, f);
+}
+
 // one product build of a loaded sequence, timed (any kernel): reps launches after one warm-up
 int pr_build(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, int reps, double *ms)
 {

@@ -42,7 +42,7 @@ L.pr_xp.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, 
 L.pr_fxp.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_int,
                      C.POINTER(D)]
 L.pr_frames_vmm.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p),
-                           C.POINTER(C.c_uint64)]
+                           C.POINTER(C.c_uint64), C.c_uint32]
 L.pr_frames_vmm_free.argtypes = [C.c_void_p, C.c_void_p]
 L.pr_frames_vmm_free.restype = None
 L.pr_xpw.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_int,
@@ -373,15 +373,16 @@ elif what == "vmm":
     f1, b1 = ctx.build_size(1, n)
     nf, nb = max(f0, f1), max(b0, b1)
     MB = 1 << 20
-    kinds = [("malloc", 0, 0), ("vmm 2M in order", 2 * MB, 0), ("vmm 2M shuffled", 2 * MB, 7),
-             ("vmm 64M in order", 64 * MB, 0), ("vmm 64M shuffled", 64 * MB, 7), ("vmm 1G shuffled", 1024 * MB, 7)]
+    kinds = [("malloc", 0, 0, 0), ("vmm 2M in order", 2 * MB, 0, 0), ("vmm 2M shuffled", 2 * MB, 7, 0),
+             ("vmm 64M in order", 64 * MB, 0, 0), ("vmm 64M shuffled", 64 * MB, 7, 0), ("vmm 1G shuffled", 1024 * MB, 7, 0),
+             ("vmm 2M in order + offsets", 2 * MB, 0, 1)]
     if os.environ.get("VMM_K"):
         keep = {int(x) for x in os.environ["VMM_K"].split(",")}
         kinds = [k for i, k in enumerate(kinds) if i in keep]
     ms = D()
     ref = None
     for alloc in range(int(os.environ.get("ALLOCS", "2"))):
-        for label, chunk, shuf in kinds:
+        for label, chunk, shuf, vflags in kinds:
             bufs = []
             t0 = time.perf_counter()
             for i in range(nbuf):
@@ -391,7 +392,7 @@ elif what == "vmm":
                     p = C.c_void_p()
                     g = C.c_uint64()
                     ok(L.pr_frames_vmm(ctx.h, nf, nb, chunk, shuf + 1000 * alloc + i if shuf else 0, C.byref(p),
-                                       C.byref(g)), label)
+                                       C.byref(g), vflags), label)
                     bufs.append(("v", p))
             t_alloc = time.perf_counter() - t0
             for i, (kind, b) in enumerate(bufs):
