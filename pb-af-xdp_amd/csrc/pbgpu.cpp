@@ -1389,12 +1389,22 @@ static hipError_t fb_alloc(const pbgpu_ctx *ctx, void **p, size_t bytes)
     size_t gran = 0;
     if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess || gran == 0 ||
         chunk % gran)
+    {
+        if (verbose())
+            fprintf(stderr, "pbgpu: allocation granularity %zu B does not divide %zu-B chunks; hipMalloc\n", gran, chunk);
+        (void)hipGetLastError();
         return hipMalloc(p, bytes);
+    }
     vmm_block B;
     B.bytes = (bytes + gran - 1) / gran * gran;
     void *va = nullptr;
     if (hipMemAddressReserve(&va, B.bytes, chunk, nullptr, 0) != hipSuccess)
+    {
+        if (verbose())
+            fprintf(stderr, "pbgpu: no %zu-B address reservation; hipMalloc\n", B.bytes);
+        (void)hipGetLastError();
         return hipMalloc(p, bytes);
+    }
     bool ok = true;
     for (size_t off = 0; off < B.bytes && ok; off += chunk)
     {
@@ -1420,10 +1430,16 @@ static hipError_t fb_alloc(const pbgpu_ctx *ctx, void **p, size_t bytes)
         ok = false;
     if (!ok)
     {
+        if (verbose())
+            fprintf(stderr, "pbgpu: chunk mapping failed after %zu chunks (%s); hipMalloc\n", B.chunks.size(),
+                    hipGetErrorString(hipGetLastError()));
         vmm_release(va, B); // the chunks mapped so far, then the reservation
         (void)hipGetLastError();
         return hipMalloc(p, bytes);
     }
+    if (verbose())
+        fprintf(stderr, "pbgpu: %zu-B buffer at %p: %zu physical chunks of <= %zu B mapped in order\n", B.bytes, va,
+                B.chunks.size(), chunk);
     {
         std::lock_guard<std::mutex> lk(g_vmm_mu);
         g_vmm.emplace(va, std::move(B));
