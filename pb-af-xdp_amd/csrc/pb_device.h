@@ -158,6 +158,14 @@ struct pb_kargs
     // sequences, {frames, bytes} for variable ones, at position pb_xcd_region(blockIdx.x); the
     // host folds them into `counters` (pb_ctr_fold).  Null: one atomic per workgroup instead.
     uint32_t *ctr_slots;
+    // pb_ximg_kernel (static-payload ICMP frames on XCD-owned pages, one wave per page): img holds
+    // the stream's first img_np pages, built at load (the static bytes repeat with that period);
+    // page c starts as a copy of page c mod img_np and each frame's IPv4 ID, TTL, checksum and
+    // source address are written over it.  Null: pb_xpage_kernel.
+    const uint32_t *img;
+    uint32_t img_np;
+    pb_div img_div;         // division by img_np
+    uint32_t img_solo;      // 1: single builds too (PBGPU_XP_IMG=2); else only pb_batch_kernel's part
 };
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)

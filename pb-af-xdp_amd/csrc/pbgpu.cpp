@@ -104,6 +104,8 @@ struct pb_opts
     bool xp_fa64 = false;    // PBGPU_XP_FA64=1: pb_xpage_kernel's 64-bit first-frame path at any size
     uint32_t xp_wgt = 0;     // PBGPU_XP_WGT: 256 / 512
     uint32_t xp_np = 0;      // PBGPU_XP_NP: pages per workgroup
+    uint32_t xp_img = 1;     // static-payload ICMP frames: 1 pb_ximg_body in pb_batch_kernel only,
+                             // 2 pb_ximg_kernel for single builds too, 0 never (PBGPU_XP_IMG)
     bool ctr_atomic = false; // PBGPU_CTR_ATOMIC=1: counts by one atomic per workgroup, no record ring
     uint32_t ctr_ring = 0;   // PBGPU_CTR_RING: record ring words (small: the fold-when-full path)
     bool batch = true;       // PBGPU_BATCH=0: pbgpu_build_batch launches every part on its own
@@ -157,6 +159,8 @@ pb_opts read_opts()
     o.xp_fa64 = opt_is("PBGPU_XP_FA64", "1");
     o.xp_wgt = opt_u32("PBGPU_XP_WGT");
     o.xp_np = opt_u32("PBGPU_XP_NP");
+    if (getenv("PBGPU_XP_IMG"))
+        o.xp_img = opt_is("PBGPU_XP_IMG", "2") ? 2u : opt_is("PBGPU_XP_IMG", "0") ? 0u : 1u;
     o.ctr_atomic = opt_is("PBGPU_CTR_ATOMIC", "1");
     o.ctr_ring = opt_u32("PBGPU_CTR_RING");
     o.batch = !opt_is("PBGPU_BATCH", "0");
@@ -201,6 +205,7 @@ struct seq_slot
     pb_pl *d_pls = nullptr;
     uint32_t *d_lit_stop = nullptr;
     uint8_t *d_blob = nullptr;
+    uint32_t *d_img = nullptr; // pb_ximg_kernel's pages (K.img)
     // per-workgroup counts of the launches not yet folded into the counters (pb_count): a
     // linear ring of u32 words, folded (pb_ctr_fold) when full, on reload and by pbgpu_counters
     uint32_t *d_ctr_slots = nullptr;
@@ -259,6 +264,7 @@ struct pbgpu_ctx
     // the shard sums {frames, bytes} per sequence, written by pb_ctr_read into mapped pinned host
     // memory (h_ctr_sum; d_ctr_sum its device address)
     unsigned long long *h_ctr_sum = nullptr, *d_ctr_sum = nullptr;
+    unsigned long long *d_img_ctr = nullptr; // counters of the load-time pb_ximg_kernel page builds (never read)
     seq_slot seqs[PB_MAX_SEQUENCES];
     std::vector<timing_pair> pending;
     std::vector<timing_pair> pool;
@@ -527,6 +533,8 @@ void slot_free(seq_slot &s)
         (void)hipFree(s.d_lit_stop);
     if (s.d_blob)
         (void)hipFree(s.d_blob);
+    if (s.d_img)
+        (void)hipFree(s.d_img);
     s = seq_slot();
 }
 
@@ -720,6 +728,8 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipFree(ctx->d_counters);
     if (ctx->h_ctr_sum)
         (void)hipHostFree(ctx->h_ctr_sum);
+    if (ctx->d_img_ctr)
+        (void)hipFree(ctx->d_img_ctr);
     if (ctx->h_stage)
         (void)hipHostFree(ctx->h_stage);
     if (ctx->d_lens)
@@ -1323,6 +1333,48 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     K.jump = ctx->d_jump;
     K.lcg48 = ctx->d_lcg48;
     K.counters = ctx->d_counters + PB_CTR_WORDS * seq_idx;
+    // pb_ximg_kernel (static-payload ICMP frames): only IPv4 ID, TTL, checksum and
+    // source address vary per frame, so the stream's bytes repeat every img_np = flen / gcd(flen,
+    // 4096) pages outside those fields.  Build its first img_np pages once, here, with
+    // pb_xpage_kernel (counted into a scratch counter array, not the sequence's)
+    if (K.xp && K.proto == 1 && !pls[0].random && K.fixed_len % 2 == 0 && O.xp_img && !O.xp_force &&
+        O.kernel == PBO_K_AUTO &&
+        !(K.flags & (PBK_RND_SPORT | PBK_RND_DPORT)))
+    {
+        uint32_t g = K.fixed_len, a = PB_XPG;
+        while (a)
+        {
+            const uint32_t t = g % a;
+            g = a;
+            a = t;
+        }
+        const uint32_t np = K.fixed_len / g;
+        const uint64_t bytes = (uint64_t)np * PB_XPG;
+        HIPCHK(hipMalloc((void **)&S.d_img, bytes));
+        if (ctx->d_img_ctr == nullptr)
+        {
+            HIPCHK(hipMalloc((void **)&ctx->d_img_ctr, PB_CTR_WORDS * sizeof(unsigned long long)));
+            HIPCHK(hipMemset(ctx->d_img_ctr, 0, PB_CTR_WORDS * sizeof(unsigned long long)));
+        }
+        pb_kargs K2 = K;
+        K2.img = nullptr;
+        K2.first_iter = 0;
+        K2.n_frames = (bytes + K.fixed_len - 1) / K.fixed_len + 1;
+        K2.total_bytes = bytes;
+        K2.out = (uint8_t *)S.d_img;
+        K2.counters = ctx->d_img_ctr;
+        K2.ctr_slots = nullptr;
+        K2.xs_nch = np;
+        K2.xs_full = np / (8 * K2.xs_np) * 8;
+        K2.xs_grid = K2.xs_full + (np - K2.xs_full * K2.xs_np + K2.xs_np - 1) / K2.xs_np;
+        K2.xp_fa_hi = 0;
+        HIPCHK(pbk_launch_build(&K2, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        K.img = S.d_img;
+        K.img_np = np;
+        K.img_div = make_div(np);
+        K.img_solo = O.xp_img == 2;
+    }
     S.K = K;
     S.opt = O;
     S.loaded = true;
@@ -1720,6 +1772,11 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
     K.xs_grid = 0;
     if (bp && K.small_ndw && K.xs_np && !K.xp) // pb_batch_kernel's 64-B part at the batch's block size
         K.xs_np = bp->wgt >> K.xs_fp_shift;
+    const bool img = K.img && (bp || K.img_solo); // pb_ximg_kernel / the batch's ICMP part
+    if (!img)
+        K.img = nullptr;
+    else // one page per wave
+        K.xs_np = (bp ? bp->wgt : PB_WG) / 64;
     if (K.small_ndw && K.xs_np && ((uintptr_t)K.out & 4095u) == 0 && S.opt.kernel != PBO_K_LINEAR)
     {
         // XCD-owned 4 KiB pages, xs_np per workgroup: pb_xsmall_kernel (one wave per page) takes
@@ -1731,7 +1788,7 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
             K.xs_nch = (uint32_t)nch;
             const uint32_t np = K.xs_np;
             K.xs_full = (uint32_t)(nch / (8 * np) * 8);
-            if (K.xp || (bp && K.small_ndw))
+            if ((K.xp || (bp && K.small_ndw)) && !K.img)
                 K.xs_grid = K.xs_full + (uint32_t)((nch - (uint64_t)K.xs_full * np + np - 1) / np);
             else
                 K.xs_grid = (uint32_t)((nch + 8ull * np - 1) / (8ull * np) * 8);
@@ -2517,9 +2574,12 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         snprintf(buf, n, "pb_stage_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
     else if (K.gpf_g)
         snprintf(buf, n, "pb_gpf_kernel<%u, %u>", K.gpf_g, K.gpf_rmode);
+    else if (K.xs_np && K.img && K.img_solo && S.opt.kernel != PBO_K_LINEAR)
+        snprintf(buf, n, "pb_ximg_kernel<%u>", (uint32_t)PB_WG);
     else if (K.xs_np && K.xp && S.opt.kernel != PBO_K_LINEAR)
-        snprintf(buf, n, "pb_xpage_kernel<%u, %u, %s, %u, %s>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
-                 K.xp_wgt, K.fixed_len % 4 == 0 ? "true" : "false");
+        snprintf(buf, n, "pb_xpage_kernel<%u, %u, %s, %u, %s>%s", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
+                 K.xp_wgt, K.fixed_len % 4 == 0 ? "true" : "false",
+                 K.img ? " (in pbgpu_build_batch: pb_ximg_body)" : "");
     else if (K.xs_np && S.opt.kernel != PBO_K_LINEAR)
         snprintf(buf, n, "pb_xsmall_kernel<%u, %u, %s, %u>", K.small_ndw, K.proto, K.pl0.random ? "true" : "false",
                  (uint32_t)PB_WG);

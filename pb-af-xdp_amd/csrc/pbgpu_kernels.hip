@@ -228,6 +228,39 @@ __device__ __forceinline__ uint2 pb_range(const pb_kargs &K, uint32_t r0)
     return K.ranges[pb_mod(r0, K.rng)];
 }
 
+// pb_header's IPv4 part alone, for pb_ximg_body (which needs no other word of the header): dwords
+// 4-7 of a frame, tot_len, ID, TTL, checksum and source address (sequence.c:443-497, 596-602);
+// l4tot = the L4 length.  The checksum also covers dword 3's high half and dword 8's low half,
+// which no random field touches (the same arithmetic as pb_header, tested against the oracle
+// with every field random, tests/test_gpu_ximg.py).
+__device__ __forceinline__ void pb_ip_words(const pb_kargs &K, uint32_t r0, uint32_t l4tot, uint2 rg, uint32_t &d4,
+                                            uint32_t &d5, uint32_t &d6, uint32_t &d7)
+{
+    const uint32_t flags = K.flags;
+    d4 = K.tmpl[4];
+    d5 = K.tmpl[5];
+    d6 = K.tmpl[6];
+    d7 = K.tmpl[7];
+    if (flags & PBK_RND_TTL) // sequence.c:443-446
+        d5 |= ((K.ttl_min + pb_mod(r0, K.ttl)) & 0xFFu) << 16;
+    if (flags & PBK_RND_ID) // sequence.c:449-452
+        d4 |= pb_bswap16((K.id_min + pb_mod(r0, K.id)) & 0xFFFFu) << 16;
+    if (flags & PBK_RND_SADDR) // sequence.c:455-497
+    {
+        const uint32_t sa = __builtin_bswap32(rg.x | (r0 & rg.y));
+        d6 |= sa << 16;
+        d7 |= sa >> 16;
+    }
+    d4 |= pb_bswap16(20u + l4tot); // tot_len, sequence.c:597
+    if (flags & PBK_IP_CSUM) // update_iph_checksum, sequence.c:599-602
+    {
+        const uint32_t sum = (K.tmpl[3] >> 16) + pb_halves(d4) + pb_halves(d5) + (d6 >> 16) + pb_halves(d7) +
+                             (K.tmpl[8] & 0xFFFFu);
+        const uint32_t c = (flags & PBK_IPH_SINGLE) ? ~((sum & 0xFFFFu) + (sum >> 16)) : ~pb_fold(sum);
+        d6 |= c & 0xFFFFu;
+    }
+}
+
 __device__ __forceinline__ uint32_t pb_header(const pb_kargs &K, uint32_t r0, uint32_t plen, uint32_t (&d)[16],
                                               uint2 rg)
 {
@@ -920,6 +953,131 @@ __global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pb_x
     pb_xpage_body<NDW, PROTO, RANDOM, WGT, A4>(K, blockIdx.x, gridDim.x, s_tile);
 }
 
+// ---------------- static-payload ICMP frames: pb_ximg_kernel ----------------
+//
+// An ICMP echo frame with a static payload (configs[4]'s 98-B frame) varies in four header fields
+// only: IPv4 ID, TTL, checksum and source address, frame bytes [18, 30) (no pseudo header: the
+// ICMP checksum is a per-sequence constant).  The stream's bytes outside those windows repeat every
+// img_np = flen / gcd(flen, 4096) pages (49 at 98 B), so pbgpu_load_sequence builds the first
+// img_np pages once (pb_xpage_kernel into K.img).  Wave w of workgroup b owns page c =
+// ((b / 8) NW + w) 8 + b % 8 (pb_xsmall_kernel's XCD ownership): it copies page c mod img_np
+// (L2-resident) into its LDS page, lane j computes frame fa + j's header fields (the first frame
+// touching the page, as pb_xpage_kernel) and writes its five 16-bit halves of [18, 30) that fall in
+// the page, and the wave stores the page as four 1-KiB instructions after a wave barrier.  Per
+// frame: the seed, rand_r and the header fields; no payload, no L4 sum, no 2-mod-4 tile write
+// (pb_xpage_kernel: 282 VALU lane-ops per 98-B frame and 49% LDS bank conflicts in its tile
+// writes, profiles/r05/prof/pmc_table.json).
+template <int WGT>
+__device__ __forceinline__ void pb_ximg_body(const pb_kargs &K, uint32_t b, uint32_t nwg, uint32_t *s_tile)
+{
+    constexpr uint32_t NW = WGT / 64;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t flen = K.fixed_len;
+    const uint64_t T = K.total_bytes;
+    const uint32_t c = ((b >> 3) * NW + w) * 8 + (b & 7u);
+    pb_u32x4 *const tile = reinterpret_cast<pb_u32x4 *>(s_tile + w * (PB_XPG / 4));
+    if (c < K.xs_nch)
+    {
+        const uint32_t q = c - pb_divq(c, K.img_div) * K.img_np;
+        const pb_u32x4 *const src = reinterpret_cast<const pb_u32x4 *>(K.img) + (size_t)q * (PB_XPG / 16);
+        pb_u32x4 v[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+            v[u] = src[u * 64 + lane];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+            tile[u * 64 + lane] = v[u];
+        // the copy before the patches (a wave's LDS operations complete in order)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint64_t fa = K.xp_fa_hi ? pb_xp_first_frame64(c, flen, K.xp_inv) : (uint64_t)pb_xp_first_frame(K, c, flen);
+        const uint32_t rem = (uint32_t)((uint64_t)c * PB_XPG - fa * flen); // < flen
+        // slots j = lane, lane + 64 (lengths under 66 B touch more than 64 frames per page)
+#pragma unroll
+        for (uint32_t p = 0; p < 2; ++p)
+        {
+            if (p && K.xp_fpp <= 64)
+                break;
+            const uint32_t j = lane + 64 * p;
+            const int off = (int)__umul24(j, flen) - (int)rem; // frame start in the page
+            const uint64_t f = fa + j;
+            if (j >= K.xp_fpp || off >= (int)PB_XPG || f >= K.n_frames)
+                continue;
+            const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + f);
+            const uint32_t r0 = pb_rand_r(s);
+            uint32_t d4, d5, d6, d7;
+            pb_ip_words(K, r0, K.l4len + flen - K.hl, pb_range(K, r0), d4, d5, d6, d7);
+            // bytes 18-19 ID, 22-23 TTL + protocol, 24-25 checksum, 26-29 source (frames start on
+            // even bytes: whole 16-bit halves)
+            const uint32_t hv[5] = {d4 >> 16, d5 >> 16, d6 & 0xFFFFu, d6 >> 16, d7 & 0xFFFFu};
+            constexpr int HB[5] = {18, 22, 24, 26, 28};
+            uint16_t *const t16 = reinterpret_cast<uint16_t *>(tile);
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+            {
+                const int pos = off + HB[i];
+                if ((uint32_t)pos < PB_XPG)
+                    t16[pos >> 1] = (uint16_t)hv[i];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint8_t *const out = K.out + (uint64_t)c * PB_XPG;
+        if ((uint64_t)(c + 1) * PB_XPG <= T) // (uniform) a whole page: no tail masks
+        {
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u)
+                pb_st16_nt(out + 16 * (u * 64 + lane), tile[u * 64 + lane]);
+        }
+        else
+        {
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u)
+            {
+                const uint32_t l = u * 64 + lane;
+                const uint64_t o = (uint64_t)c * PB_XPG + 16 * l;
+                if (o < T)
+                {
+                    pb_u32x4 x = tile[l];
+                    if (o + 16 > T) // last chunk of the stream: zero the tail
+                    {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            x[t] &= pb_range_mask(0, (int)(T - o) - 4 * t);
+                    }
+                    pb_st16_nt(out + 16 * l, x);
+                }
+            }
+        }
+    }
+    if (threadIdx.x == 0)
+    {
+        // the workgroup's pages ascend with i: all whole unless the last one reaches the stream end
+        const uint32_t cl = ((b >> 3) * NW + NW - 1) * 8 + (b & 7u);
+        uint64_t by = (uint64_t)NW * PB_XPG;
+        if ((uint64_t)(cl + 1) * PB_XPG > T)
+        {
+            by = 0;
+            for (uint32_t i = 0; i < NW; ++i)
+            {
+                const uint32_t ci = ((b >> 3) * NW + i) * 8 + (b & 7u);
+                if (ci < K.xs_nch)
+                    by += min((uint64_t)PB_XPG, T - (uint64_t)ci * PB_XPG);
+            }
+        }
+        pb_count_at(K, b, pb_xcd_region(b, nwg), 0, by);
+    }
+}
+
+template <int WGT>
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_num_sgpr(80))) void pb_ximg_kernel(pb_kargs K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[(WGT / 64) * (PB_XPG / 4)];
+    pb_ximg_body<WGT>(K, blockIdx.x, gridDim.x, s_tile);
+}
+
 // ---------------- several sequences in one launch: pb_batch_kernel ----------------
 //
 // configs[4] builds three sequences per step (64-B UDP, 60-B TCP SYN, 98-B ICMP), each a launch
@@ -946,6 +1104,8 @@ __device__ __forceinline__ void pb_batch_part(const pb_kargs &K, uint32_t b, uin
         pb_xsmall_wg_body<WGT>(K, b, nwg, s_tile);
     else if constexpr (KIND == 2)
         pb_xpage_body<16, 6, true, WGT, true>(K, b, nwg, s_tile);
+    else if (K.img)
+        pb_ximg_body<WGT>(K, b, nwg, s_tile);
     else
         pb_xpage_body<32, 1, false, WGT, false>(K, b, nwg, s_tile);
 }
@@ -2823,6 +2983,11 @@ static void pbk_launch_linear(const pb_kargs *K, hipStream_t st)
 template <int NDW, int PROTO>
 static void pbk_launch_small_p(const pb_kargs *K, uint32_t grid, hipStream_t st)
 {
+    if (K->xs_grid && K->img && K->img_solo)
+    {
+        hipLaunchKernelGGL((pb_ximg_kernel<PB_WG>), dim3(K->xs_grid), dim3(PB_WG), K->lds_pad, st, *K);
+        return;
+    }
     if (K->xs_grid && K->xp)
     {
         const size_t lds = (size_t)K->xs_np * PB_XREG + K->lds_pad;
@@ -2910,7 +3075,8 @@ extern "C" hipError_t pbk_launch_batch(const pb_kargs *Ks, uint32_t wgt, hipStre
         A.K[j] = Ks[j];
         A.g[j] = Ks[j].xs_grid;
         grid += j < 2 ? (A.g[j] + 7u) & ~7u : A.g[j];
-        const size_t l = (size_t)(j == 0 ? wgt / 64u : Ks[j].xs_np) * PB_XREG; // (the parts' own caps do not apply)
+        const size_t l = Ks[j].img ? (size_t)(wgt / 64u) * PB_XPG // (the parts' own caps do not apply)
+                                   : (size_t)(j == 0 ? wgt / 64u : Ks[j].xs_np) * PB_XREG;
         lds = l > lds ? l : lds;
     }
     if (wgt == 512)

@@ -695,6 +695,14 @@ __global__ __launch_bounds__(256) void pr_fxp_kernel(pb_kargs K, uint32_t ns)
     }
 }
 
+// pb_ximg_body without the SGPR budget
+template <int WGT>
+__global__ __launch_bounds__(WGT) void pr_ximg_nos80(pb_kargs K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[(WGT / 64) * (PB_XPG / 4)];
+    pb_ximg_body<WGT>(K, blockIdx.x, gridDim.x, s_tile);
+}
+
 // ---------------------------------------------------------------- write-only fill shapes
 // persistent XCD-owned page walker: NPP pages per step (workgroup b on XCD b % 8 takes pages
 // (m NPP + p) 8 + x, m = t Wx + j)
@@ -1269,6 +1277,43 @@ void pr_frames_vmm_free(pbgpu_ctx *ctx, pbgpu_frames *f)
             break;
         }
     pbgpu_frames_free(ctx, f);
+}
+
+// pb_ximg_kernel shapes on a loaded static-payload ICMP sequence: 0 the product launch (as
+// loaded), 1 pb_ximg_kernel<256> with lds_pad dynamic LDS, 2 <512>, 3 <128>, 4 <256> without the
+// SGPR budget, 5 <512> without it
+int pr_ximg(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, int variant,
+            uint32_t lds_pad, int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr_kargs(ctx, seq, first, n, out, 256, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    PB_JOIN(ctx);
+    if (!K.xs_grid || !K.img)
+        return PBGPU_EINVAL;
+    hipStream_t st = ctx->stream;
+    static const uint32_t WG[6] = {256, 256, 512, 128, 256, 512};
+    if (variant < 0 || variant > 5)
+        return PBGPU_EINVAL;
+    const uint32_t nw = WG[variant] / 64;
+    const dim3 g((K.xs_nch + 8 * nw - 1) / (8 * nw) * 8);
+    pb_kargs K2 = K;
+    K2.xs_np = nw;
+    auto launch = [&]() -> hipError_t {
+        switch (variant)
+        {
+        case 0: return pbk_launch_build(&K, st);
+        case 1: hipLaunchKernelGGL((pb_ximg_kernel<256>), g, dim3(256), lds_pad, st, K2); break;
+        case 2: hipLaunchKernelGGL((pb_ximg_kernel<512>), g, dim3(512), lds_pad, st, K2); break;
+        case 3: hipLaunchKernelGGL((pb_ximg_kernel<128>), g, dim3(128), lds_pad, st, K2); break;
+        case 4: hipLaunchKernelGGL((pr_ximg_nos80<256>), g, dim3(256), lds_pad, st, K2); break;
+        case 5: hipLaunchKernelGGL((pr_ximg_nos80<512>), g, dim3(512), lds_pad, st, K2); break;
+        }
+        return hipGetLastError();
+    };
+    return pr_time_launches(ctx, reps, ms, launch);
 }
 
 // one product build of a loaded sequence, timed (any kernel): reps launches after one warm-up

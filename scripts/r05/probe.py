@@ -45,6 +45,8 @@ L.pr_frames_vmm.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_
                            C.POINTER(C.c_uint64), C.c_uint32]
 L.pr_frames_vmm_free.argtypes = [C.c_void_p, C.c_void_p]
 L.pr_frames_vmm_free.restype = None
+L.pr_ximg.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_int,
+                      C.POINTER(D)]
 L.pr_xpw.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.c_uint32, C.c_int,
                      C.POINTER(D)]
 
@@ -426,6 +428,41 @@ elif what == "vmm":
                     b.free()
                 else:
                     L.pr_frames_vmm_free(ctx.h, b)
+
+elif what == "ximg":
+    # pb_ximg_kernel shapes (block size, occupancy cap by dynamic LDS, SGPR budget) on NBUF 98-B
+    # ICMP buffers, beside pb_xpage_kernel (sequence slot 1, loaded with PBGPU_XP_IMG=0 semantics
+    # through a second context); each shape checked against the product launch first
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "3"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c5_icmp_echo")), pc.SEED_BASE)
+    os.environ["PBGPU_XP_IMG"] = "0"  # slot 1: the same sequence on pb_xpage_kernel
+    ctx.load_sequence(1, Sequence.from_config(pc.get("c5_icmp_echo")), pc.SEED_BASE)
+    del os.environ["PBGPU_XP_IMG"]
+    bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(nbuf)]
+    ms = D()
+    names = {0: "product", 1: "w256", 2: "w512", 3: "w128", 4: "w256 nos80", 5: "w512 nos80"}
+    spec = os.environ.get("XIMG_V", "0:0,1:0,1:40000,1:30000,1:25000,2:0,2:60000,2:45000,3:0,3:20000,4:0,4:30000,5:0")
+    V = [(int(a), int(b)) for a, b in (x.split(":") for x in spec.split(","))]
+    ok(L.pr_ximg(ctx.h, 0, 5, n, bufs[1].ptr, 0, 0, 1, C.byref(ms)), "ref")
+    for v in sorted({v for v, _ in V if v}):
+        ok(L.pr_ximg(ctx.h, 0, 5, n, bufs[0].ptr, v, 0, 1, C.byref(ms)), names[v])
+        bad = C.c_uint64()
+        ok(L.pr_compare(ctx.h, C.c_void_p(data_ptr(bufs[0])), C.c_void_p(data_ptr(bufs[1])), n * 98, C.byref(bad)),
+           "cmp")
+        emit({"check": names[v], "bad_dwords": bad.value})
+    ramp(lambda: L.pr_ximg(ctx.h, 0, 0, n, bufs[0].ptr, 0, 0, 8, C.byref(ms)))
+    for r in range(REPS):
+        for i, fb in enumerate(bufs):
+            row = {"rep": r, "buf": i}
+            for v, pad in V:
+                ok(L.pr_ximg(ctx.h, 0, 0, n, fb.ptr, v, pad, 20, C.byref(ms)), names[v])
+                row[names[v] + (f" lds{pad}" if pad else "")] = round(ms.value, 5)
+            ok(L.pr_build(ctx.h, 1, 0, n, fb.ptr, 20, C.byref(ms)), "xpage")
+            row["pb_xpage_kernel"] = round(ms.value, 5)
+            emit(row)
+    for fb in bufs:
+        fb.free()
 
 elif what == "detect":
     # can a short probe at allocation time tell a slow placement?  Region vs page fills over

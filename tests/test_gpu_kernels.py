@@ -148,14 +148,18 @@ XS_LENS = [42, 43, 44, 48, 52, 56, 60, 64, 72, 96, 98, 100, 106, 108, 116, 120, 
 XS_COUNTS = [1, 5, 200, 2048, 2049, 2 * 2048 * 5 + 77]
 
 
-@pytest.mark.parametrize("force_xpage", [False, True, 512, "lin64", "lin128", "fa64"],
+@pytest.mark.parametrize("force_xpage", [False, True, 512, "lin64", "lin128", "fa64", "img"],
                          ids=["default", "xpage_forced", "xpage_forced_512", "linear_wg64", "linear_wg128",
-                              "xpage_forced_fa64"])
+                              "xpage_forced_fa64", "ximg_single_builds"])
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
 @pytest.mark.parametrize("flen", XS_LENS)
 def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
     if force_xpage == "fa64":  # pb_xpage_kernel's 64-bit first-frame path at every size
         monkeypatch.setenv("PBGPU_XP_FA64", "1")
+    solo = force_xpage == "img"  # static-payload ICMP frames on pb_ximg_kernel in single builds too
+    if solo:
+        monkeypatch.setenv("PBGPU_XP_IMG", "2")
+        force_xpage = False
     if force_xpage:
         monkeypatch.setenv("PBGPU_XP_FORCE", "1")
     if force_xpage == 512:
@@ -180,8 +184,12 @@ def test_small_frames_pages(ctx, monkeypatch, proto, flen, force_xpage):
         kern = _check(ctx, cfg, 1000003 + n, n)
         # pbgpu_load_sequence: 52-64 B multiples of 4; static payloads at even 52-128 B
         xp_default = 52 <= flen <= 64 and flen % 4 == 0 or (proto == "icmp" and 52 <= flen <= 128)
+        # pb_ximg_kernel (PBGPU_XP_IMG=2): static-payload ICMP frames on the page kernel's pages
+        img = proto == "icmp" and flen % 2 == 0 and solo and 4096 % flen and xp_default
         if lin:
             want = "pb_small_kernel<"
+        elif img:
+            want = "pb_ximg_kernel"
         elif flen % 2 == 0 and (force_xpage or (4096 % flen and xp_default)):
             want = "pb_xpage_kernel"
         else:
