@@ -21,9 +21,17 @@ for d in sorted(glob.glob(os.path.join(out_dir, "pmc_*"))):
             cfg = name[: -len(tag)]
     for f in glob.glob(os.path.join(d, "run_counter_collection.csv")):
         agg = collections.defaultdict(list)
-        for r in csv.DictReader(open(f)):
+        rows = list(csv.DictReader(open(f)))
+        isbuild = lambda kn: kn.startswith("void pb_") and any(  # noqa: E731
+            x in kn for x in ("gpf", "stage", "small", "xpage", "ximg", "vline", "batch", "fpage"))
+        # the build launches are the largest build-kernel grid; smaller ones are setup dispatches
+        # (pb_ximg_body's image pages, built once by pb_xpage_kernel at load)
+        gmax = max([int(r["Grid_Size"]) for r in rows if isbuild(r["Kernel_Name"])] or [0])
+        for r in rows:
             kn = r["Kernel_Name"]
-            build = kn.startswith("void pb_") and any(x in kn for x in ("gpf", "stage", "small", "xpage", "vline", "batch", "fpage"))
+            build = isbuild(kn)
+            if build and int(r["Grid_Size"]) < gmax:
+                continue
             aux = kn.startswith("void pb_len_") or kn.startswith("pb_len_") or "pb_scan_blocks" in kn
             fold = "pb_ctr_fold" in kn  # the counters' fold: its bytes spread over the build launches
             aux = aux or fold

@@ -14,9 +14,14 @@ for f in glob.glob(os.path.join(sys.argv[1], "pmc_*", "**", "*counter_collection
     cfg = os.path.relpath(f, sys.argv[1]).split(os.sep)[0][4:]
     for g in ("_WRITE_SIZE", "_FETCH_SIZE", "_G1", "_G2", "_G3"):
         cfg = cfg[: -len(g)] if cfg.endswith(g) else cfg
-    for r in csv.DictReader(open(f)):
+    rows = list(csv.DictReader(open(f)))
+    want = lambda kn: kn.startswith("void pb_") and "len_" not in kn and "scan" not in kn and "fill" not in kn  # noqa
+    # the build launches: the largest grid (smaller ones are setup dispatches, e.g. pb_ximg_body's
+    # image pages built at load)
+    gmax = max([int(r["Grid_Size"]) for r in rows if want(r["Kernel_Name"])] or [0])
+    for r in rows:
         kn = r["Kernel_Name"]
-        if kn.startswith("void pb_") and "len_" not in kn and "scan" not in kn and "fill" not in kn:
+        if want(kn) and int(r["Grid_Size"]) == gmax:
             out[(cfg, kn.split("(")[0][5:])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 res = {}
 for (cfg, kn), cs in sorted(out.items()):
