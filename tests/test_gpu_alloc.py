@@ -34,8 +34,12 @@ def _build(monkeypatch, name, n, malloc):
             umem.tobytes(), lens.tobytes(), int(p[0]), int(b[0]))
 
 
+@pytest.mark.parametrize("chunk_mb", [None, 2])
 @pytest.mark.parametrize("name,n", [("c2_udp_64", 1 << 22), ("c3_udp_var", 1 << 19)])
-def test_chunk_mapped_buffer_matches_hipmalloc(monkeypatch, name, n):
+def test_chunk_mapped_buffer_matches_hipmalloc(monkeypatch, name, n, chunk_mb):
+    """The default 64-MiB chunks and 2-MiB ones (PBGPU_ALLOC_CHUNK_MB)."""
+    if chunk_mb:
+        monkeypatch.setenv("PBGPU_ALLOC_CHUNK_MB", str(chunk_mb))
     a = _build(monkeypatch, name, n, malloc=False)
     b = _build(monkeypatch, name, n, malloc=True)
     assert a == b
