@@ -34,12 +34,15 @@ def _build(monkeypatch, name, n, malloc):
             umem.tobytes(), lens.tobytes(), int(p[0]), int(b[0]))
 
 
-@pytest.mark.parametrize("chunk_mb", [None, 2])
+@pytest.mark.parametrize("chunk_mb,dma", [(None, False), (2, False), (None, True)])
 @pytest.mark.parametrize("name,n", [("c2_udp_64", 1 << 22), ("c3_udp_var", 1 << 19)])
-def test_chunk_mapped_buffer_matches_hipmalloc(monkeypatch, name, n, chunk_mb):
-    """The default 64-MiB chunks and 2-MiB ones (PBGPU_ALLOC_CHUNK_MB)."""
+def test_chunk_mapped_buffer_matches_hipmalloc(monkeypatch, name, n, chunk_mb, dma):
+    """The default 64-MiB chunks, 2-MiB ones (PBGPU_ALLOC_CHUNK_MB), and UMEM landing through DMA
+    copies from them (PBGPU_UMEM_DMA=1) instead of the mapped scatter kernel."""
     if chunk_mb:
         monkeypatch.setenv("PBGPU_ALLOC_CHUNK_MB", str(chunk_mb))
+    if dma:
+        monkeypatch.setenv("PBGPU_UMEM_DMA", "1")
     a = _build(monkeypatch, name, n, malloc=False)
     b = _build(monkeypatch, name, n, malloc=True)
     assert a == b
