@@ -1,13 +1,20 @@
 """Round-5 A/B probe driver (lib/libpbprobe.so from tools/r05_probe.hip; tool only).
 
-python3 scripts/r05/probe.py xs|xs8|xs9|xsapi|xp|mix|place|detect|wfill|capx [reps]
+python3 scripts/r05/probe.py MODE [reps]
 (the pb_fpage_kernel modes "fpage" / "fpord" are in commit 37dc421 with the kernel)
-  xs     64-B page-kernel shapes and the decomposition (full / stores only / arithmetic only /
-         the 4-KiB fill) on one buffer, variants alternating; wave-local shapes checked
-         byte for byte against the product launch
-  mix    configs[4]'s fused-launch variants on three buffers
-  place  the packed (configs[2]) and 1500-B kernels and write-only fill shapes on several
-         large buffers alive at once (each keeps its physical placement)
+  xs / xs8 / xs9 / xsapi   64-B page-kernel shapes, the decomposition (full / stores only /
+         arithmetic only / the 4-KiB fill), occupancy caps, count records; wave-local shapes
+         checked byte for byte against the product launch
+  xp / xpw   60-B / 98-B page kernels: SGPR budget, page-store shapes (wave-owned pages,
+         wave-local builds)
+  mix    configs[4]'s fused-launch variants on three buffers (MIX_V selects)
+  ximg   the static-payload ICMP image kernel's block sizes / caps beside pb_xpage_kernel
+  fxp    a page-owned 1500-B writer on pb_fstage_kernel's frame machinery, with decomposition
+  place / detect / wfill / capx   the region kernels and write-only fill shapes on several large
+         buffers alive at once (each keeps its physical placement); sub-range placement probes;
+         occupancy caps
+  vmm    frame buffers from physical chunks (hipMemCreate) mapped in order or shuffled vs
+         hipMalloc, re-allocated ALLOCS times
 One JSON line per measurement."""
 import ctypes as C
 import json
