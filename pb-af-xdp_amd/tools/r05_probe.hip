@@ -6,8 +6,11 @@
 //   * 64-B page-kernel shapes: wave-local pages (no workgroup barrier), one-wave workgroups,
 //     persistent page walkers; decomposition variants (stores only, arithmetic only);
 //   * configs[4] fused-launch variants;
+//   * 60-B / 98-B page-store shapes (pr_xpw), the static-payload ICMP image kernel's shapes
+//     (pr_ximg), a page-owned 1500-B writer on pb_fstage_kernel's machinery (pr_fxp);
 //   * write-only fill shapes over a caller's buffer (placement study: persistent XCD-owned
-//     page walkers vs region writers).
+//     page walkers vs region writers), and frame buffers built from physical chunks
+//     (pr_frames_vmm: hipMemCreate chunks mapped in order or shuffled).
 // Built by scripts/r05/build_probe.sh into lib/libpbprobe.so; driven by scripts/r05/probe.py.
 #include "../csrc/pbgpu_kernels.hip"
 #include "../csrc/pbgpu.cpp"
