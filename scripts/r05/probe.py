@@ -15,6 +15,8 @@ python3 scripts/r05/probe.py MODE [reps]
          occupancy caps
   vmm    frame buffers from physical chunks (hipMemCreate) mapped in order or shuffled vs
          hipMalloc, re-allocated ALLOCS times
+  remap  allocation-time detection (whole-buffer region / page fill ratio) and replacement of
+         buffers that draw the slow placement
 One JSON line per measurement."""
 import ctypes as C
 import json
@@ -468,6 +470,55 @@ elif what == "ximg":
             ok(L.pr_build(ctx.h, 1, 0, n, fb.ptr, 20, C.byref(ms)), "xpage")
             row["pb_xpage_kernel"] = round(ms.value, 5)
             emit(row)
+    for fb in bufs:
+        fb.free()
+
+elif what == "remap":
+    # can a buffer that draws the slow placement be replaced at allocation time?  NBUF configs[2]
+    # buffers (library allocation, chunk-mapped by default); each one's whole-buffer region-fill /
+    # page-fill ratio (the detection) and configs[2] time; a buffer under RATIO gets up to TRIES
+    # replacement allocations (held while trying, so each lands on other pages), the first one
+    # at or over RATIO kept
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "4"))
+    thr = float(os.environ.get("RATIO", "0.99"))
+    tries = int(os.environ.get("TRIES", "3"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
+    f0, b0 = ctx.build_size(0, n)
+    ms = D()
+
+    def measure(fb):
+        ok(L.pr_build(ctx.h, 0, 0, n, fb.ptr, 5, C.byref(ms)), "c3")
+        c3 = ms.value
+        tot = int(b0) // 16 * 16
+        ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), tot, 1, 2048, 5, C.byref(ms)), "reg")
+        reg = tot / (ms.value * 1e-3) / 1e12
+        ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), tot, 0, 2048, 5, C.byref(ms)), "page")
+        page = tot / (ms.value * 1e-3) / 1e12
+        return {"c3_ms": round(c3, 4), "reg_tbps": round(reg, 3), "page_tbps": round(page, 3),
+                "ratio": round(reg / page, 4), "addr": hex(data_ptr(fb))}
+
+    bufs = [ctx.alloc_frames(f0, b0) for _ in range(nbuf)]
+    ramp(lambda: L.pr_build(ctx.h, 0, 0, n, bufs[0].ptr, 2, C.byref(ms)))
+    for i in range(nbuf):
+        m = measure(bufs[i])
+        emit({"buf": i, "try": 0, **m})
+        held = []
+        t = 0
+        while m["ratio"] < thr and t < tries:
+            t += 1
+            nb = ctx.alloc_frames(f0, b0)
+            m = measure(nb)
+            emit({"buf": i, "try": t, **m})
+            if m["ratio"] >= thr:
+                bufs[i].free()
+                bufs[i] = nb
+            else:
+                held.append(nb)
+        for h in held:
+            h.free()
+    for i, fb in enumerate(bufs):
+        emit({"buf": i, "final": True, **measure(fb)})
     for fb in bufs:
         fb.free()
 
