@@ -13,11 +13,12 @@ from pbgpu import LIB_PATH, GpuContext, Sequence  # noqa: E402
 
 var = os.path.join(ROOT, sys.argv[1])
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 17
-ENVS = [{}, {"PBGPU_STAGE_KB": "16"}, {"PBGPU_FST_DBG": "16"}, {"PBGPU_FST_DBG": "32"}]
+ENVS = [{}, {"PBGPU_STAGE_KB": "16"}, {"PBGPU_FST_G": "16"}, {"PBGPU_FST_G": "32"},
+        {"PBGPU_XP_IMG": "2"}, {"PBGPU_XP_IMG": "0"}, {"PBGPU_ALLOC": "malloc"}]
 ctxs = [GpuContext(0, lib_path=LIB_PATH), GpuContext(0, lib_path=var)]
 bad = 0
 for env in ENVS:
-    for k in ("PBGPU_STAGE_KB", "PBGPU_FST_DBG"):
+    for k in ("PBGPU_STAGE_KB", "PBGPU_FST_G", "PBGPU_XP_IMG", "PBGPU_ALLOC"):
         os.environ.pop(k, None)
     os.environ.update(env)
     for name in pc.ALL:

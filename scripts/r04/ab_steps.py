@@ -43,7 +43,7 @@ def run(tag, nb, env, k):
         os.environ.pop(key, None)
     os.environ.update(env)
     ctx = ctxs[tag]
-    for i, nm in enumerate(names):  # load-time switches (PBGPU_FST_DBG, shapes) take effect
+    for i, nm in enumerate(names):  # load-time switches (PBGPU_FST_G and the other shapes) take effect
         ctx.load_sequence(i, Sequence.from_config(pc.get(nm)), pc.SEED_BASE)
     bufs = [[ctx.alloc_frames(*ctx.build_size(i, n)) for i in range(len(names))] for _ in range(nb)]
     def step(first, row):

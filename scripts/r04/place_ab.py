@@ -37,7 +37,7 @@ for rnd in range(int(os.environ.get("ROUNDS", "2"))):
             for key in keys:
                 os.environ.pop(key, None)
             os.environ.update(env)
-            ctx.load_sequence(0, seq, pc.SEED_BASE)  # load-time switches (PBGPU_FST_DBG) take effect
+            ctx.load_sequence(0, seq, pc.SEED_BASE)  # load-time switches (PBGPU_FST_G, PBGPU_XP_IMG) take effect
             for s in range(k):
                 ctx.build(0, s * n, n, fb)
             ctx.sync()
