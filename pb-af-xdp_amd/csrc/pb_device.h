@@ -23,6 +23,7 @@
 #define PB_XREG (PB_XPG + 256)             // LDS bytes per page region (128 B slack either side)
 #define PBK_FILL_SHAPES 15                 // write-roofline probe shapes (pbk_launch_fill)
 #define PB_XNP_MAX 8                       // pb_xsmall_kernel: pages per workgroup, 4 (64-B frames) or 8 (128-B)
+#define PB_VL_GRP 32                       // length pass: build workgroups per group sum (vblk_l2 entry)
 #ifndef PB_CTR_SHARDS
 #define PB_CTR_SHARDS 64                   // per-sequence counter shards (workgroup b adds to shard b % 64)
 #endif
@@ -131,7 +132,7 @@ struct pb_kargs
                             // bit 8 no longest-first window order
     uint32_t lds_pad;       // dynamic LDS added to the build launch: caps its workgroups per CU
     // pb_vstage_kernel, variable length: per-workgroup length sums (stage_wgf frames each) and
-    // their exclusive scan per 256 workgroups (pb_len_wgsum + pb_scan_blocks); the kernel then
+    // their exclusive scan per PB_VL_GRP workgroups (pb_len_wgsum + pb_scan_blocks); the kernel then
     // writes offsets_w for its own frames.  Null: offsets[] was scanned beforehand (3 passes).
     const uint32_t *vblk_sum;
     const unsigned long long *vblk_l2;

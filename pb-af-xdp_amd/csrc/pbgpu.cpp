@@ -55,7 +55,7 @@ extern "C" hipError_t pbk_launch_scatter_fixed(const uint8_t *src, uint32_t flen
 #define PB_CTR_BYTES (sizeof(unsigned long long) * PB_CTR_WORDS * PB_MAX_SEQUENCES)
 
 // device scratch of a frames buffer: the 3-pass length scan's block sums, or pb_vstage_kernel's
-// per-workgroup length sums (u32) + their per-256 group sums (u64)
+// per-workgroup length sums (u32) + their per-PB_VL_GRP group sums (u64)
 static uint64_t vst_bsum_bytes(uint64_t nblk)
 {
     return (nblk * 4 + 15) & ~15ull;
@@ -64,7 +64,7 @@ static uint64_t scan_tmp_bytes(uint64_t capacity_frames)
 {
     const uint64_t a = (capacity_frames / PB_SCAN_FRAMES_PER_BLOCK + 1) * 8;
     const uint64_t nblk = capacity_frames / PB_VST_SCAN_MIN_WGF + 1;
-    const uint64_t b = vst_bsum_bytes(nblk) + (nblk / 256 + 1) * 8;
+    const uint64_t b = vst_bsum_bytes(nblk) + (nblk / PB_VL_GRP + 1) * 8;
     return a > b ? a : b;
 }
 
@@ -1741,7 +1741,7 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
             // pb_vline_kernel / pb_vstage_kernel: per-workgroup length sums, their scan, offsets
             // written by the build
             const uint64_t nblk = (nf + wgf - 1) / wgf;
-            const uint64_t n_l2 = (nblk + 255) / 256;
+            const uint64_t n_l2 = (nblk + PB_VL_GRP - 1) / PB_VL_GRP;
             uint32_t *bsum = reinterpret_cast<uint32_t *>(out->scan_tmp);
             unsigned long long *l2 =
                 reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(out->scan_tmp) + vst_bsum_bytes(nblk));

@@ -1977,13 +1977,13 @@ __global__ __launch_bounds__(PB_WG) void pb_vstage_kernel(pb_kargs K)
     constexpr uint32_t GH = PB_VST_GHOSTS;
     const int64_t fb = (int64_t)f0 - (int64_t)GH;
     // start of frame f0: fixed length, or the scanned per-workgroup length sums (l2 prefix of
-    // this workgroup's group of 256 + the sums of the earlier workgroups of the group), or
+    // this workgroup's group of PB_VL_GRP + the sums of the earlier workgroups of the group), or
     // offsets[] when the 3-pass scan ran
     const bool bsum = !K.fixed_len && K.vblk_sum != nullptr;
     uint64_t s0_part = 0;
-    if (bsum && tid < (bxr & 255u))
-        s0_part = K.vblk_sum[(bxr & ~255u) + tid];
-    const uint64_t s0_base = K.fixed_len ? f0 * K.fixed_len : (bsum ? K.vblk_l2[bxr >> 8] : K.offsets[f0]);
+    if (bsum && tid < (bxr & (PB_VL_GRP - 1u)))
+        s0_part = K.vblk_sum[(bxr & ~(PB_VL_GRP - 1u)) + tid];
+    const uint64_t s0_base = K.fixed_len ? f0 * K.fixed_len : (bsum ? K.vblk_l2[bxr / PB_VL_GRP] : K.offsets[f0]);
     uint2 jtv = make_uint2(0u, 0u);
     if (tid < 16u) // state at payload index -((r % 16) + hl): the first byte of the frame's first chunk
         jtv = K.jump[PB_JNEG - (tid + hl)];
@@ -2545,9 +2545,9 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     // ---------------- prologue: one lane per frame slot ----------------
     const int64_t fb = (int64_t)f0 - (int64_t)GH;
     uint64_t s0_part = 0;
-    if (tid < (bxr & 255u))
-        s0_part = K.vblk_sum[(bxr & ~255u) + tid];
-    const uint64_t s0_base = K.vblk_l2[bxr >> 8];
+    if (tid < (bxr & (PB_VL_GRP - 1u)))
+        s0_part = K.vblk_sum[(bxr & ~(PB_VL_GRP - 1u)) + tid];
+    const uint64_t s0_base = K.vblk_l2[bxr / PB_VL_GRP];
     uint2 jtv = make_uint2(0u, 0u);
     if (tid < 16u)
         jtv = K.jump[PB_JNEG - (tid + HL)];
@@ -2803,32 +2803,76 @@ __global__ __launch_bounds__(256) void pb_len_reduce(pb_kargs K, unsigned long l
         block_sums[blockIdx.x] = s_part[0];
 }
 
-// single workgroup: exclusive scan of the block sums in place
+// single workgroup: exclusive scan of the block sums in place, in passes of 8192 entries: coalesced
+// loads into LDS (one pad word per 8 entries), 8 consecutive entries per lane, one shuffle scan per
+// wave, the wave sums through LDS, coalesced stores.  A pass waits on its loads' latency (the sums
+// were written by every XCD), so the passes are few: the length pass's group sums are
+// 2^25 / 252 / PB_VL_GRP = 4,161 entries at configs[2]'s size, one pass.  (Strided per-lane loads or
+// a chain of 64-bit row scans took 12-20 us for 8,322 entries, 4-entry passes 14 us.)
 __global__ __launch_bounds__(1024) void pb_scan_blocks(unsigned long long *block_sums, uint32_t nblocks,
                                                        uint64_t *offsets, uint64_t n_frames)
 {
-    __shared__ unsigned long long s_v[1024];
+    constexpr uint32_t IT = 8, PASS = 1024 * IT;
+    __shared__ unsigned long long s_v[PASS + PASS / 8];
+    __shared__ unsigned long long s_w[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     unsigned long long carry = 0;
-    for (uint32_t base = 0; base < nblocks; base += 1024)
+    for (uint32_t base = 0; base < nblocks; base += PASS)
     {
-        const uint32_t i = base + threadIdx.x;
-        const unsigned long long v = i < nblocks ? block_sums[i] : 0ull;
-        s_v[threadIdx.x] = v;
-        __syncthreads();
-        for (uint32_t d = 1; d < 1024; d <<= 1)
+        const uint32_t n = nblocks - base < PASS ? nblocks - base : PASS;
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k)
         {
-            const unsigned long long t = threadIdx.x >= d ? s_v[threadIdx.x - d] : 0ull;
-            __syncthreads();
-            s_v[threadIdx.x] += t;
-            __syncthreads();
+            const uint32_t i = k * 1024 + tid;
+            s_v[i + (i >> 3)] = i < n ? block_sums[base + i] : 0ull;
         }
-        if (i < nblocks)
-            block_sums[i] = carry + s_v[threadIdx.x] - v;
-        const unsigned long long tot = s_v[1023];
         __syncthreads();
+        const uint32_t p0 = tid * (IT + 1); // IT consecutive entries, no pad among them
+        unsigned long long v[IT], t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k)
+        {
+            v[k] = s_v[p0 + k];
+            t += v[k];
+        }
+        unsigned long long x = t; // inclusive scan of the lanes' sums within the wave
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1)
+        {
+            const unsigned long long y = __shfl_up(x, d, 64);
+            if (lane >= d)
+                x += y;
+        }
+        if (lane == 63u)
+            s_w[w] = x;
+        __syncthreads();
+        unsigned long long wpre = 0, tot = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j)
+        {
+            const unsigned long long sj = s_w[j];
+            wpre += j < w ? sj : 0ull;
+            tot += sj;
+        }
+        unsigned long long run = carry + wpre + x - t;
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k)
+        {
+            s_v[p0 + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k)
+        {
+            const uint32_t i = k * 1024 + tid;
+            if (i < n)
+                block_sums[base + i] = s_v[i + (i >> 3)];
+        }
         carry += tot;
+        __syncthreads(); // s_v and s_w are rewritten by the next pass
     }
-    if (threadIdx.x == 0)
+    if (tid == 0)
         offsets[n_frames] = carry; // (the build kernels count frames and bytes as they store them)
 }
 
@@ -3257,25 +3301,35 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
     return hipGetLastError();
 }
 
-// pb_vstage_kernel's length pass: lane b sums the lengths of workgroup b's wgf frames
-// (bsum[b]), each 256-lane group the sums of its 256 workgroups (l2[group], scanned next
-// by pb_scan_blocks); the build kernel writes offsets[] itself
+// pb_vline_kernel's / pb_vstage_kernel's length pass: workgroup g sums the lengths of build
+// workgroups [PB_VL_GRP g, PB_VL_GRP (g + 1)), 256 / PB_VL_GRP lanes per build workgroup, frames
+// dealt round-robin to them (bsum[b]: build workgroup b's sum; l2[g]: the group's sum, scanned
+// next by pb_scan_blocks).  One lane per build workgroup (252 frames in a row, 2 workgroups per
+// CU with a third on some) took 0.090 ms per 2^25 frames (profiles/r05/prof/cfg/), 16 lanes 0.069-0.072.
 __global__ __launch_bounds__(256) void pb_len_wgsum(pb_kargs K, uint32_t wgf, uint32_t nblk, uint32_t *bsum,
                                                     unsigned long long *l2)
 {
-    __shared__ unsigned long long s_w[4];
-    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    constexpr uint32_t LPB = PB_WG / PB_VL_GRP; // lanes per build workgroup
+    static_assert(LPB >= 1 && LPB <= 64 && (LPB & (LPB - 1)) == 0, "PB_VL_GRP: a power of 2 in [4, 256]");
+    __shared__ unsigned long long s_w[PB_WG / 64];
+    const uint32_t b = blockIdx.x * PB_VL_GRP + threadIdx.x / LPB;
+    const uint32_t sub = threadIdx.x & (LPB - 1u);
     uint32_t sum = 0;
     if (b < nblk)
     {
         const uint64_t fa = (uint64_t)b * wgf;
         const uint64_t fz = fa + wgf < K.n_frames ? fa + wgf : K.n_frames;
 #pragma unroll 4
-        for (uint64_t f = fa; f < fz; ++f)
+        for (uint64_t f = fa + sub; f < fz; f += LPB)
             sum += pb_frame_len<false>(K, f);
-        bsum[b] = sum;
     }
-    unsigned long long v = sum;
+#pragma unroll
+    for (uint32_t dd = LPB / 2; dd > 0; dd >>= 1)
+        sum += __shfl_xor(sum, dd, 64);
+    if (b < nblk && sub == 0)
+        bsum[b] = sum;
+    // group sum: every lane group's sum once (its first lane)
+    unsigned long long v = sub == 0 ? sum : 0u;
 #pragma unroll
     for (uint32_t dd = 32; dd > 0; dd >>= 1)
         v += __shfl_xor(v, dd, 64);
@@ -3283,13 +3337,19 @@ __global__ __launch_bounds__(256) void pb_len_wgsum(pb_kargs K, uint32_t wgf, ui
         s_w[threadIdx.x >> 6] = v;
     __syncthreads();
     if (threadIdx.x == 0)
-        l2[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    {
+        unsigned long long t = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < PB_WG / 64; ++i)
+            t += s_w[i];
+        l2[blockIdx.x] = t;
+    }
 }
 
 extern "C" hipError_t pbk_launch_vst_lengths(const pb_kargs *K, uint32_t wgf, uint32_t *bsum, uint32_t nblk,
                                              unsigned long long *l2, uint32_t n_l2, uint64_t *offsets, hipStream_t st)
 {
-    hipLaunchKernelGGL(pb_len_wgsum, dim3(n_l2), dim3(256), 0, st, *K, wgf, nblk, bsum, l2);
+    hipLaunchKernelGGL(pb_len_wgsum, dim3(n_l2), dim3(PB_WG), 0, st, *K, wgf, nblk, bsum, l2);
     hipLaunchKernelGGL(pb_scan_blocks, dim3(1), dim3(1024), 0, st, l2, n_l2, offsets, K->n_frames);
     return hipGetLastError();
 }
