@@ -495,8 +495,13 @@ elif what == "remap":
         reg = tot / (ms.value * 1e-3) / 1e12
         ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), tot, 0, 2048, 5, C.byref(ms)), "page")
         page = tot / (ms.value * 1e-3) / 1e12
-        return {"c3_ms": round(c3, 4), "reg_tbps": round(reg, 3), "page_tbps": round(page, 3),
-                "ratio": round(reg / page, 4), "addr": hex(data_ptr(fb))}
+        r = {"c3_ms": round(c3, 4), "reg_tbps": round(reg, 3), "page_tbps": round(page, 3),
+             "ratio": round(reg / page, 4), "addr": hex(data_ptr(fb))}
+        for sh in (int(x) for x in os.environ.get("XSHAPES", "").split(",") if x):
+            # extra detection candidates: XCD-contiguous fills (2: 96 KiB per workgroup, 7: 24 KiB)
+            ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), tot, sh, 2048, 5, C.byref(ms)), f"s{sh}")
+            r[f"s{sh}_ratio"] = round(tot / (ms.value * 1e-3) / 1e12 / page, 4)
+        return r
 
     bufs = [ctx.alloc_frames(f0, b0) for _ in range(nbuf)]
     ramp(lambda: L.pr_build(ctx.h, 0, 0, n, bufs[0].ptr, 2, C.byref(ms)))
