@@ -1331,6 +1331,96 @@ int pr_build(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_fra
     return pr_time_launches(ctx, reps, ms, [&] { return pbk_launch_build(&K, ctx->stream); });
 }
 
+// plain stores in the packed kernel's geometry (tool only): workgroup b writes region
+// pb_xcd_region(b) = [rstart[r] & ~127, rstart[r + 1] & ~127) of a finished configs[2] build in 16-KiB
+// steps, wave w bytes [4 KiB w, 4 KiB (w + 1)) of a step as four 1-KiB instructions.
+// MODE 0: as the kernel (non-temporal); 1: region edges rounded down to 4 KiB; 2: equal regions
+// (the mean size, 128-B multiple); 3: as 0 with plain stores; 4: as 0 with blockIdx-ordered regions
+extern "C++" {
+template <int MODE>
+__global__ __launch_bounds__(256) void pr_fill_vgeom(uint8_t *dst, const unsigned long long *rstart, uint32_t nreg,
+                                                     uint64_t total)
+{
+    const uint32_t b = blockIdx.x;
+    const uint32_t r = MODE == 4 ? b : pb_xcd_region(b, gridDim.x);
+    const uint64_t mask = MODE == 1 ? ~4095ull : ~127ull;
+    uint64_t lo, hi;
+    if (MODE == 2)
+    {
+        const uint64_t sz = (total / nreg) & ~127ull;
+        lo = (uint64_t)r * sz;
+        hi = r + 1 < nreg ? lo + sz : total;
+    }
+    else
+    {
+        lo = r ? (rstart[r] & mask) : 0ull;
+        hi = r + 1 < nreg ? (rstart[r + 1] & mask) : total;
+    }
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const pb_u32x4 v = {b, lane, 0x5EEDu, 0xBA5Eu};
+    for (uint64_t st = lo; st < hi; st += 16384)
+    {
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+        {
+            const uint64_t o = st + 4096 * w + 1024 * u + 16 * lane;
+            if (o < hi)
+            {
+                if (MODE == 3)
+                    pb_st16(dst + o, v);
+                else
+                    pb_st16_nt(dst + o, v);
+            }
+        }
+    }
+}
+} // extern "C++"
+
+int pr_fill_vgeom_run(pbgpu_ctx *ctx, pbgpu_frames *out, uint32_t nreg, uint64_t total, int mode, int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    frames_events *fe = frames_ev(out);
+    if (fe == nullptr || fe->d_rstart == nullptr || nreg == 0)
+        return PBGPU_EINVAL;
+    uint8_t *d = (uint8_t *)out->data;
+    const unsigned long long *rs = fe->d_rstart;
+    hipStream_t st = ctx->stream;
+    return pr_time_launches(ctx, reps, ms, [&] {
+        switch (mode)
+        {
+        case 0: hipLaunchKernelGGL(pr_fill_vgeom<0>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 1: hipLaunchKernelGGL(pr_fill_vgeom<1>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 2: hipLaunchKernelGGL(pr_fill_vgeom<2>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 3: hipLaunchKernelGGL(pr_fill_vgeom<3>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        default: hipLaunchKernelGGL(pr_fill_vgeom<4>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        }
+        return hipGetLastError();
+    });
+}
+
+// the packed kernel building into out's frame bytes while writing offs's 4-B offsets and region
+// starts (and reading its length sums): does the slow placement follow the data or the offsets?
+int pr_build_swap(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, pbgpu_frames *offs,
+                  int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K, K2;
+    int rc = pr_kargs(ctx, seq, first, n, offs, 256, &K2);
+    if (rc != PBGPU_OK)
+        return rc;
+    rc = pr_kargs(ctx, seq, first, n, out, 256, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    if (!K.vl)
+        return PBGPU_EINVAL;
+    K.offsets32 = K2.offsets32;
+    K.vl_rstart = K2.vl_rstart;
+    K.vblk_sum = K2.vblk_sum;
+    K.vblk_l2 = K2.vblk_l2;
+    PB_JOIN(ctx);
+    return pr_time_launches(ctx, reps, ms, [&] { return pbk_launch_build(&K, ctx->stream); });
+}
+
 // a product build with its workgroups per CU capped at per_cu by dynamic LDS (0: as loaded)
 int pr_build_cap(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, uint32_t per_cu,
                  int reps, double *ms, uint32_t *base_lds)

@@ -15,6 +15,9 @@ python3 scripts/r05/probe.py MODE [reps]
          occupancy caps
   vmm    frame buffers from physical chunks (hipMemCreate) mapped in order or shuffled vs
          hipMalloc, re-allocated ALLOCS times
+  offswap  configs[2] with each buffer's frame bytes and every buffer's offset arrays; with VGEOM=1
+         instead the packed kernel's store geometry as plain fills (pr_fill_vgeom modes), and with
+         VTOTALS=b,b,... equal-region fills beside the page fill over the first b bytes
   remap  allocation-time detection (whole-buffer region / page fill ratio) and replacement of
          buffers that draw the slow placement
 One JSON line per measurement."""
@@ -40,6 +43,9 @@ L.pr_xs.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, 
 L.pr_mix.argtypes = [C.c_void_p, C.POINTER(C.c_uint16), C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p), C.c_int,
                      C.c_int, C.POINTER(D)]
 L.pr_build.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.POINTER(D)]
+L.pr_fill_vgeom_run.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.POINTER(D)]
+L.pr_build_swap.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int,
+                            C.POINTER(D)]
 L.pr_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_uint32, C.c_int, C.POINTER(D)]
 L.pr_fill_name.restype = C.c_char_p
 L.pr_compare.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
@@ -524,6 +530,49 @@ elif what == "remap":
             h.free()
     for i, fb in enumerate(bufs):
         emit({"buf": i, "final": True, **measure(fb)})
+    for fb in bufs:
+        fb.free()
+
+elif what == "offswap":
+    # does configs[2]'s slow placement follow the frame bytes or the 4-B offset arrays?  NBUF
+    # buffers alive at once; the packed kernel timed for every (data buffer, offsets buffer) pair,
+    # ROUNDS times
+    n = 1 << 25
+    nbuf = int(os.environ.get("NBUF", "3"))
+    ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
+    f0, b0 = ctx.build_size(0, n)
+    ms = D()
+    bufs = [ctx.alloc_frames(f0, b0) for _ in range(nbuf)]
+    ramp(lambda: L.pr_build(ctx.h, 0, 0, n, bufs[0].ptr, 2, C.byref(ms)))
+    if os.environ.get("VGEOM"):
+        # the kernel's store geometry as plain fills (pr_fill_vgeom modes), per buffer, beside the build
+        wf = 252
+        nreg = (n + wf - 1) // wf
+        for rnd in range(int(os.environ.get("ROUNDS", "2"))):
+            for i, fb in enumerate(bufs):
+                ok(L.pr_build(ctx.h, 0, 0, n, fb.ptr, 3, C.byref(ms)), "c3")
+                row = {"round": rnd, "buf": i, "c3_ms": round(ms.value, 4)}
+                tot = int(os.environ.get("VTOTAL", "27649414866"))  # configs[2]'s bytes at first 0, 2^25 frames
+                for mode in range(5):
+                    ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, nreg, tot, mode, 5, C.byref(ms)), "vgeom")
+                    row[f"g{mode}_ms"] = round(ms.value, 4)
+                for t2 in (int(x) for x in os.environ.get("VTOTALS", "").split(",") if x):
+                    # equal 208-KiB regions over the first t2 bytes, and the page fill over them
+                    nr2 = (t2 + 212991) // 212992
+                    ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, nr2, t2, 2, 5, C.byref(ms)), "vgeom2")
+                    g2 = ms.value
+                    ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), t2 // 16 * 16, 0, 2048, 5, C.byref(ms)), "page")
+                    row[f"t{t2 >> 30}G"] = {"g2_ms": round(g2, 4), "page_ms": round(ms.value, 4),
+                                           "ratio": round(g2 / ms.value, 3)}
+                emit(row)
+        for fb in bufs:
+            fb.free()
+        sys.exit(0)
+    for rnd in range(int(os.environ.get("ROUNDS", "2"))):
+        for i in range(nbuf):
+            for j in range(nbuf):
+                ok(L.pr_build_swap(ctx.h, 0, 0, n, bufs[i].ptr, bufs[j].ptr, 5, C.byref(ms)), "swap")
+                emit({"round": rnd, "data": i, "offs": j, "ms": round(ms.value, 4)})
     for fb in bufs:
         fb.free()
 
