@@ -1342,10 +1342,31 @@ __global__ __launch_bounds__(256) void pr_fill_vgeom(uint8_t *dst, const unsigne
                                                      uint64_t total)
 {
     const uint32_t b = blockIdx.x;
-    const uint32_t r = MODE == 4 ? b : pb_xcd_region(b, gridDim.x);
+    uint32_t r = MODE == 4 ? b : pb_xcd_region(b, gridDim.x);
+    const uint32_t per = gridDim.x >> 3;
+    if (MODE >= 5 && b < 8u * per)
+    {
+        const uint32_t x = b & 7u, k = b >> 3;
+        uint32_t kk = k;
+        if (MODE == 5) // odd XCDs walk their eighth backwards
+            kk = (x & 1u) ? per - 1u - k : k;
+        else if (MODE == 6) // XCD x starts x/8 of the way into its eighth and wraps
+            kk = (k + x * (per >> 3)) % per;
+        else if (MODE == 7) // two fronts per XCD: its workgroups alternate between the halves
+            kk = (k & 1u) ? (per >> 1) + (k >> 1) : (k >> 1);
+        if (MODE == 8) // 16 fronts: XCD x owns sixteenths x and x + 8, alternating
+        {
+            const uint32_t h = per >> 1;
+            r = (k & 1u) ? (x + 8u) * h + (k >> 1) : x * h + (k >> 1);
+            if ((k >> 1) >= h)
+                r = x * per + k; // (odd per: the leftover, as MODE 2)
+        }
+        else
+            r = x * per + kk;
+    }
     const uint64_t mask = MODE == 1 ? ~4095ull : ~127ull;
     uint64_t lo, hi;
-    if (MODE == 2)
+    if (MODE == 2 || MODE >= 5)
     {
         const uint64_t sz = (total / nreg) & ~127ull;
         lo = (uint64_t)r * sz;
@@ -1392,7 +1413,11 @@ int pr_fill_vgeom_run(pbgpu_ctx *ctx, pbgpu_frames *out, uint32_t nreg, uint64_t
         case 1: hipLaunchKernelGGL(pr_fill_vgeom<1>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
         case 2: hipLaunchKernelGGL(pr_fill_vgeom<2>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
         case 3: hipLaunchKernelGGL(pr_fill_vgeom<3>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
-        default: hipLaunchKernelGGL(pr_fill_vgeom<4>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 4: hipLaunchKernelGGL(pr_fill_vgeom<4>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 5: hipLaunchKernelGGL(pr_fill_vgeom<5>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 6: hipLaunchKernelGGL(pr_fill_vgeom<6>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 7: hipLaunchKernelGGL(pr_fill_vgeom<7>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        default: hipLaunchKernelGGL(pr_fill_vgeom<8>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
         }
         return hipGetLastError();
     });

@@ -559,11 +559,12 @@ elif what == "offswap":
                 for t2 in (int(x) for x in os.environ.get("VTOTALS", "").split(",") if x):
                     # equal 208-KiB regions over the first t2 bytes, and the page fill over them
                     nr2 = (t2 + 212991) // 212992
-                    ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, nr2, t2, 2, 5, C.byref(ms)), "vgeom2")
-                    g2 = ms.value
                     ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), t2 // 16 * 16, 0, 2048, 5, C.byref(ms)), "page")
-                    row[f"t{t2 >> 30}G"] = {"g2_ms": round(g2, 4), "page_ms": round(ms.value, 4),
-                                           "ratio": round(g2 / ms.value, 3)}
+                    e = {"page_ms": round(ms.value, 4)}
+                    for mode in [int(x) for x in os.environ.get("VMODES", "2").split(",")]:
+                        ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, nr2, t2, mode, 5, C.byref(ms)), "vgeom2")
+                        e[f"m{mode}"] = round(ms.value / e["page_ms"], 3)
+                    row[f"t{t2 >> 30}G"] = e
                 emit(row)
         for fb in bufs:
             fb.free()
