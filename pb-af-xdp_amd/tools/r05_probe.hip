@@ -1335,16 +1335,17 @@ int pr_build(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_fra
 // pb_xcd_region(b) = [rstart[r] & ~127, rstart[r + 1] & ~127) of a finished configs[2] build in 16-KiB
 // steps, wave w bytes [4 KiB w, 4 KiB (w + 1)) of a step as four 1-KiB instructions.
 // MODE 0: as the kernel (non-temporal); 1: region edges rounded down to 4 KiB; 2: equal regions
-// (the mean size, 128-B multiple); 3: as 0 with plain stores; 4: as 0 with blockIdx-ordered regions
+// (the mean size, 128-B multiple); 3: as 0 with plain stores; 4: as 0 with blockIdx-ordered regions;
+// 5-8: equal regions, other XCD walks (below); 9: equal regions in blockIdx order
 extern "C++" {
 template <int MODE>
 __global__ __launch_bounds__(256) void pr_fill_vgeom(uint8_t *dst, const unsigned long long *rstart, uint32_t nreg,
                                                      uint64_t total)
 {
     const uint32_t b = blockIdx.x;
-    uint32_t r = MODE == 4 ? b : pb_xcd_region(b, gridDim.x);
+    uint32_t r = (MODE == 4 || MODE == 9) ? b : pb_xcd_region(b, gridDim.x);
     const uint32_t per = gridDim.x >> 3;
-    if (MODE >= 5 && b < 8u * per)
+    if (MODE >= 5 && MODE <= 8 && b < 8u * per)
     {
         const uint32_t x = b & 7u, k = b >> 3;
         uint32_t kk = k;
@@ -1417,7 +1418,8 @@ int pr_fill_vgeom_run(pbgpu_ctx *ctx, pbgpu_frames *out, uint32_t nreg, uint64_t
         case 5: hipLaunchKernelGGL(pr_fill_vgeom<5>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
         case 6: hipLaunchKernelGGL(pr_fill_vgeom<6>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
         case 7: hipLaunchKernelGGL(pr_fill_vgeom<7>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
-        default: hipLaunchKernelGGL(pr_fill_vgeom<8>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 8: hipLaunchKernelGGL(pr_fill_vgeom<8>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        default: hipLaunchKernelGGL(pr_fill_vgeom<9>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
         }
         return hipGetLastError();
     });

@@ -561,9 +561,17 @@ elif what == "offswap":
                     nr2 = (t2 + 212991) // 212992
                     ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), t2 // 16 * 16, 0, 2048, 5, C.byref(ms)), "page")
                     e = {"page_ms": round(ms.value, 4)}
-                    for mode in [int(x) for x in os.environ.get("VMODES", "2").split(",")]:
+                    for mode in [int(x) for x in os.environ.get("VMODES", "2").split(",") if x]:
                         ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, nr2, t2, mode, 5, C.byref(ms)), "vgeom2")
                         e[f"m{mode}"] = round(ms.value / e["page_ms"], 3)
+                    for kib in [int(x) for x in os.environ.get("VREG", "").split(",") if x]:
+                        # equal regions of kib KiB (contiguous eighths)
+                        ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, t2 // (kib << 10), t2, 2, 5, C.byref(ms)), "vreg")
+                        e[f"r{kib}K"] = round(ms.value / e["page_ms"], 3)
+                    for kib in [int(x) for x in os.environ.get("VREG9", "").split(",") if x]:
+                        # equal regions of kib KiB in blockIdx order (consecutive regions on different XCDs)
+                        ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, t2 // (kib << 10), t2, 9, 5, C.byref(ms)), "vreg9")
+                        e[f"b{kib}K"] = round(ms.value / e["page_ms"], 3)
                     row[f"t{t2 >> 30}G"] = e
                 emit(row)
         for fb in bufs:
