@@ -1400,8 +1400,8 @@ int pbgpu_build_size(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t n_iter, uint64_t
 // (hipMemCreate, alloc_chunk_mb each) mapped in creation order into one reserved VA range,
 // instead of one hipMalloc: the region kernels' slow mode follows the buffer's
 // physical placement; in fresh processes hipMalloc drew it 3 times in 4 (pb_fstage_kernel 8.47 ms,
-// pb_vline_kernel 5.06-5.08) and chunk-mapped buffers never in 8 (7.24-7.30 / 4.36-4.40;
-// profiles/r05/ab/alloc_ab2.jsonl, vmm*.jsonl).  Falls back to hipMalloc when the virtual-memory
+// pb_vline_kernel 5.06-5.08) and chunk-mapped buffers 2 times in 40 (7.24-7.30 / 4.36-4.40 otherwise;
+// profiles/r05/ab/alloc_ab2.jsonl, vmm*.jsonl, lenpass_ab.log).  Falls back to hipMalloc when the virtual-memory
 // calls fail.  The blocks are kept in a process-wide table, so fb_free needs no context; callers
 // free only after the work that uses a block has completed (pbgpu_frames_free synchronises first).
 #define PB_VMM_MIN (64ull << 20)
