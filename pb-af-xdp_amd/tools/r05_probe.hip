@@ -1398,6 +1398,14 @@ __global__ __launch_bounds__(256) void pr_fill_vgeom(uint8_t *dst, const unsigne
 }
 } // extern "C++"
 
+// the product's write-probe shapes (pbk_launch_fill modes) over one range, timed
+int pr_fill_prod(pbgpu_ctx *ctx, void *dst, uint64_t bytes, int mode, int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    return pr_time_launches(ctx, reps, ms, [&] { return pbk_launch_fill(dst, bytes, mode, st); });
+}
+
 int pr_fill_vgeom_run(pbgpu_ctx *ctx, pbgpu_frames *out, uint32_t nreg, uint64_t total, int mode, int reps, double *ms)
 {
     HIPCHK(hipSetDevice(ctx->device));

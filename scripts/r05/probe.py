@@ -44,6 +44,7 @@ L.pr_mix.argtypes = [C.c_void_p, C.POINTER(C.c_uint16), C.c_uint64, C.c_uint64, 
                      C.c_int, C.POINTER(D)]
 L.pr_build.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int, C.POINTER(D)]
 L.pr_fill_vgeom_run.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.POINTER(D)]
+L.pr_fill_prod.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.POINTER(D)]
 L.pr_build_swap.argtypes = [C.c_void_p, C.c_uint16, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int,
                             C.POINTER(D)]
 L.pr_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_uint32, C.c_int, C.POINTER(D)]
@@ -568,6 +569,14 @@ elif what == "offswap":
                         # equal regions of kib KiB (contiguous eighths)
                         ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, t2 // (kib << 10), t2, 2, 5, C.byref(ms)), "vreg")
                         e[f"r{kib}K"] = round(ms.value / e["page_ms"], 3)
+                    for m in [int(x) for x in os.environ.get("VPROD", "").split(",") if x]:
+                        # the product's write-probe shapes (pbk_launch_fill modes)
+                        ok(L.pr_fill_prod(ctx.h, C.c_void_p(data_ptr(fb)), t2 // 16 * 16, m, 5, C.byref(ms)), "prod")
+                        e[f"p{m}"] = round(ms.value / e["page_ms"], 3)
+                    for sh in [int(x) for x in os.environ.get("VPR", "").split(",") if x]:
+                        # the probe's own fill shapes (pr_fill: 8, 9 XCD-owned pages as pb_xsmall_kernel)
+                        ok(L.pr_fill(ctx.h, C.c_void_p(data_ptr(fb)), t2 // 16 * 16, sh, 2048, 5, C.byref(ms)), "pr")
+                        e[f"s{sh}"] = round(ms.value / e["page_ms"], 3)
                     for kib in [int(x) for x in os.environ.get("VREG9", "").split(",") if x]:
                         # equal regions of kib KiB in blockIdx order (consecutive regions on different XCDs)
                         ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, t2 // (kib << 10), t2, 9, 5, C.byref(ms)), "vreg9")
