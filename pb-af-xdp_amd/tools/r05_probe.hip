@@ -1336,13 +1336,41 @@ int pr_build(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_fra
 // steps, wave w bytes [4 KiB w, 4 KiB (w + 1)) of a step as four 1-KiB instructions.
 // MODE 0: as the kernel (non-temporal); 1: region edges rounded down to 4 KiB; 2: equal regions
 // (the mean size, 128-B multiple); 3: as 0 with plain stores; 4: as 0 with blockIdx-ordered regions;
-// 5-8: equal regions, other XCD walks (below); 9: equal regions in blockIdx order
+// 5-8: equal regions, other XCD walks (below); 9: equal regions in blockIdx order; 10, 11: window-
+// coherent walks (below)
 extern "C++" {
 template <int MODE>
 __global__ __launch_bounds__(256) void pr_fill_vgeom(uint8_t *dst, const unsigned long long *rstart, uint32_t nreg,
                                                      uint64_t total)
 {
     const uint32_t b = blockIdx.x;
+    if (MODE == 10 || MODE == 11)
+    {
+        // window-coherent walk: XCD x's eighth in units of 4 KiB (10) or 16 KiB (11); the XCD's k-th
+        // workgroup writes units k, k + per, k + 2 per, ... so its resident workgroups write adjacent units
+        constexpr uint64_t U = MODE == 10 ? 4096 : 16384;
+        const uint32_t per = gridDim.x >> 3;
+        if (b >= 8u * per)
+            return;
+        const uint32_t x = b & 7u, k = b >> 3;
+        const uint64_t eighth = (total / 8) & ~(U - 1);
+        const uint64_t nun = eighth / U;
+        const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+        const pb_u32x4 v = {b, lane, 0x5EEDu, 0xBA5Eu};
+        for (uint64_t u = k; u < nun; u += per)
+        {
+            uint8_t *const q = dst + (uint64_t)x * eighth + u * U;
+            if (MODE == 10)
+                pb_st16_nt(q + 16 * threadIdx.x, v);
+            else
+            {
+#pragma unroll
+                for (uint32_t c = 0; c < 4; ++c)
+                    pb_st16_nt(q + 4096 * w + 1024 * c + 16 * lane, v);
+            }
+        }
+        return;
+    }
     uint32_t r = (MODE == 4 || MODE == 9) ? b : pb_xcd_region(b, gridDim.x);
     const uint32_t per = gridDim.x >> 3;
     if (MODE >= 5 && MODE <= 8 && b < 8u * per)
@@ -1427,7 +1455,9 @@ int pr_fill_vgeom_run(pbgpu_ctx *ctx, pbgpu_frames *out, uint32_t nreg, uint64_t
         case 6: hipLaunchKernelGGL(pr_fill_vgeom<6>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
         case 7: hipLaunchKernelGGL(pr_fill_vgeom<7>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
         case 8: hipLaunchKernelGGL(pr_fill_vgeom<8>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
-        default: hipLaunchKernelGGL(pr_fill_vgeom<9>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 9: hipLaunchKernelGGL(pr_fill_vgeom<9>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        case 10: hipLaunchKernelGGL(pr_fill_vgeom<10>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
+        default: hipLaunchKernelGGL(pr_fill_vgeom<11>, dim3(nreg), dim3(256), 0, st, d, rs, nreg, total); break;
         }
         return hipGetLastError();
     });

@@ -569,6 +569,11 @@ elif what == "offswap":
                         # equal regions of kib KiB (contiguous eighths)
                         ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, t2 // (kib << 10), t2, 2, 5, C.byref(ms)), "vreg")
                         e[f"r{kib}K"] = round(ms.value / e["page_ms"], 3)
+                    for g in [int(x) for x in os.environ.get("VWIN", "").split(",") if x]:
+                        # window-coherent walks (modes 10: 4-KiB units, 11: 16-KiB units) with a grid of g
+                        for mode in (10, 11):
+                            ok(L.pr_fill_vgeom_run(ctx.h, fb.ptr, g, t2, mode, 5, C.byref(ms)), "vwin")
+                            e[f"w{mode}g{g}"] = round(ms.value / e["page_ms"], 3)
                     for m in [int(x) for x in os.environ.get("VPROD", "").split(",") if x]:
                         # the product's write-probe shapes (pbk_launch_fill modes)
                         ok(L.pr_fill_prod(ctx.h, C.c_void_p(data_ptr(fb)), t2 // 16 * 16, m, 5, C.byref(ms)), "prod")
