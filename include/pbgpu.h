@@ -181,7 +181,7 @@ int pbgpu_kernel_times(pbgpu_ctx *ctx, double *ms_each, uint32_t cap, uint32_t *
  * PBGPU_FILL_SHAPES fill shapes over `bytes` — 16-B stores per lane at 16 / 4 /
  * 8 KiB per workgroup, plain and non-temporal, workgroups per CU capped by LDS, linear or
  * XCD-contiguous workgroup regions,
- * and the runtime's hipMemsetD32Async (tools/wbench.hip found the fastest plain
+ * and the runtime's hipMemsetD32Async (probes/wbench.hip found the fastest plain
  * fills).  pbgpu_fill_probe returns the fastest shape's mean
  * device time per launch; _ex returns every shape's and the fastest's index,
  * pbgpu_fill_shape_name names a shape. */

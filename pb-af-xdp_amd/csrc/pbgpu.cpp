@@ -1065,7 +1065,9 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
             K.xs_np = 256 >> K.xs_fp_shift;
             // one wave per page is fastest with few waves per CU (profiles/r05/ab/xs9.jsonl):
             // 64-B frames 0.297-0.303 ms per 2^25 at 3 workgroups per CU, 0.323-0.329 uncapped
-            K.lds_pad = lds_cap_pad(K.xs_np * PB_XPG, PB_XS_WG_PER_CU);
+            // (measured for 64-B frames only; 128-B pages keep the uncapped launch)
+            if (K.xs_fp_shift == 6)
+                K.lds_pad = lds_cap_pad(K.xs_np * PB_XPG, PB_XS_WG_PER_CU);
         }
         else if ((xp_force && minf % 2 == 0) ||
                  (O.kernel != PBO_K_NOPAGE && minf % 2 == 0 && minf >= 52 && minf <= 128 &&
@@ -1411,6 +1413,7 @@ namespace
 struct vmm_block
 {
     size_t bytes;
+    int device; // the GPU whose memory the chunks are (fb_free synchronises it before unmapping)
     std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks; // handle, size
 };
 std::mutex g_vmm_mu;
@@ -1450,6 +1453,7 @@ static hipError_t fb_alloc(const pbgpu_ctx *ctx, void **p, size_t bytes)
     }
     vmm_block B;
     B.bytes = (bytes + gran - 1) / gran * gran;
+    B.device = ctx->device;
     void *va = nullptr;
     if (hipMemAddressReserve(&va, B.bytes, chunk, nullptr, 0) != hipSuccess)
     {
@@ -1501,6 +1505,9 @@ static hipError_t fb_alloc(const pbgpu_ctx *ctx, void **p, size_t bytes)
     return hipSuccess;
 }
 
+// hipFree waits for the device; unmapping does not, so a chunk-mapped block first waits for every
+// stream of its device (work queued on a caller's stream, or a free without a context, must not
+// find its pages gone: a GPU page fault instead of hipFree's implicit wait)
 static void fb_free(void *p)
 {
     if (p == nullptr)
@@ -1510,6 +1517,12 @@ static void fb_free(void *p)
         auto it = g_vmm.find(p);
         if (it != g_vmm.end())
         {
+            int cur = -1;
+            (void)hipGetDevice(&cur);
+            if (hipSetDevice(it->second.device) == hipSuccess)
+                (void)hipDeviceSynchronize();
+            if (cur >= 0)
+                (void)hipSetDevice(cur);
             vmm_release(p, it->second);
             g_vmm.erase(it);
             return;
@@ -1797,10 +1810,12 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
             K.xp_fa_hi = K.xp && ((uint64_t)nch * (4096 % K.fixed_len) >= (1ull << 31) || S.opt.xp_fa64);
         }
     }
+    // the load-time occupancy cap (lds_pad) belongs to pb_xsmall_kernel's page launch alone: the
+    // linear fallback (an output not 4-KiB aligned, PBGPU_KERNEL=linear) keeps its own occupancy
+    if (K.xs_grid == 0)
+        K.lds_pad = 0;
     timing_pair tp = {nullptr, nullptr};
     int rc = PBGPU_OK;
-    if (!bp && !span && (rc = timed_pair(ctx, &tp)) != PBGPU_OK)
-        return rc;
     // this launch's per-workgroup count records (pb_count): the next words of the sequence's
     // ring, folded into the counters first when it is full (PBGPU_CTR_ATOMIC=1: one atomic per
     // workgroup instead).  Reserved last, after everything that can fail but the launch itself;
@@ -1842,17 +1857,33 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
         bp->ctr_words = words;
         return PBGPU_OK;
     }
-    hipError_t le = hipSuccess;
+    // every error exit from here on returns the reserved count-ring words (their records would
+    // never be written, and the next fold would read stale ones) and the timing pair
+    auto undo = [&]() {
+        S.ctr_used -= words;
+        if (tp.a)
+            ctx->pool.push_back(tp);
+    };
+#define HIPCHK_UNDO(call)                                                                    \
+    do                                                                                       \
+    {                                                                                        \
+        const hipError_t u_ = (call);                                                        \
+        if (u_ != hipSuccess)                                                                \
+        {                                                                                    \
+            undo();                                                                          \
+            HIPCHK(u_);                                                                      \
+        }                                                                                    \
+    } while (0)
     if (span)
     {
         if (ctx->span_n == 0)
         {
             if (ctx->span.a == nullptr)
             {
-                HIPCHK(hipEventCreate(&ctx->span.a));
-                HIPCHK(hipEventCreate(&ctx->span.b));
+                HIPCHK_UNDO(hipEventCreate(&ctx->span.a));
+                HIPCHK_UNDO(hipEventCreate(&ctx->span.b));
             }
-            HIPCHK(hipEventRecord(ctx->span.a, ctx->stream));
+            HIPCHK_UNDO(hipEventRecord(ctx->span.a, ctx->stream));
             for (bool &j : ctx->seq_in_span)
                 j = false;
         }
@@ -1860,28 +1891,24 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
         {
             if (!ctx->seq_in_span[si]) // the span starts before this stream's first launch in it
             {
-                HIPCHK(hipStreamWaitEvent(st, ctx->span.a, 0));
+                HIPCHK_UNDO(hipStreamWaitEvent(st, ctx->span.a, 0));
                 ctx->seq_in_span[si] = true;
             }
             ctx->seq_dirty[si] = true;
         }
-        le = pbk_launch_build(&K, st);
-        if (le != hipSuccess)
-        {
-            S.ctr_used -= words;
-            HIPCHK(le);
-        }
+        HIPCHK_UNDO(pbk_launch_build(&K, st));
         ++ctx->span_n;
         return mark_built(ctx, out, st);
     }
-    HIPCHK(hipEventRecord(tp.a, ctx->stream));
-    le = pbk_launch_build(&K, ctx->stream);
-    if (le != hipSuccess)
+    if ((rc = timed_pair(ctx, &tp)) != PBGPU_OK)
     {
-        S.ctr_used -= words;
-        ctx->pool.push_back(tp);
-        HIPCHK(le);
+        undo();
+        return rc;
     }
+    HIPCHK_UNDO(hipEventRecord(tp.a, ctx->stream));
+    HIPCHK_UNDO(pbk_launch_build(&K, ctx->stream));
+#undef HIPCHK_UNDO
+    // launched: its records will be written; a failing end event drops only this timing
     HIPCHK(hipEventRecord(tp.b, ctx->stream));
     if ((rc = mark_built(ctx, out, st)) != PBGPU_OK)
         return rc;
@@ -1990,25 +2017,32 @@ int pbgpu_build_batch(pbgpu_ctx *ctx, uint32_t n, const uint16_t *seq_idx, const
         }
         Ks[k] = bp[k].K;
     }
+    // (every error exit from here to the launch returns the three parts' reservations)
+#define HIPCHK_UNRES(call)                                                                   \
+    do                                                                                       \
+    {                                                                                        \
+        const hipError_t u_ = (call);                                                        \
+        if (u_ != hipSuccess)                                                                \
+        {                                                                                    \
+            unreserve(3);                                                                    \
+            HIPCHK(u_);                                                                      \
+        }                                                                                    \
+    } while (0)
     if (span && ctx->span_n == 0)
     {
         if (ctx->span.a == nullptr)
         {
-            HIPCHK(hipEventCreate(&ctx->span.a));
-            HIPCHK(hipEventCreate(&ctx->span.b));
+            HIPCHK_UNRES(hipEventCreate(&ctx->span.a));
+            HIPCHK_UNRES(hipEventCreate(&ctx->span.b));
         }
-        HIPCHK(hipEventRecord(ctx->span.a, ctx->stream));
+        HIPCHK_UNRES(hipEventRecord(ctx->span.a, ctx->stream));
         for (bool &j : ctx->seq_in_span)
             j = false;
     }
     if (!span)
-        HIPCHK(hipEventRecord(tp.a, st));
-    const hipError_t le = pbk_launch_batch(Ks, ctx->opt.batch_wgt, st);
-    if (le != hipSuccess)
-    {
-        unreserve(3);
-        HIPCHK(le);
-    }
+        HIPCHK_UNRES(hipEventRecord(tp.a, st));
+    HIPCHK_UNRES(pbk_launch_batch(Ks, ctx->opt.batch_wgt, st));
+#undef HIPCHK_UNRES
     if (span)
         ++ctx->span_n;
     else

@@ -2444,13 +2444,49 @@ constexpr uint32_t PB_A3I = pb_inv24(PB_A3 & PB_M24);
 constexpr uint32_t PB_C3I = (0u - PB_A3I * (PB_C3 & PB_M24)) & PB_M24;
 static_assert(((PB_A3I * (PB_A3 & PB_M24)) & PB_M24) == 1u, "M^-1");
 
+// x * a (low 24 bits of each), one v_mul_u32_u24 with both operands in VGPRs
+__device__ __forceinline__ uint32_t pb_mul24v(uint32_t x, uint32_t a)
+{
+    uint32_t r;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(x), "v"(a));
+    return r;
+}
+
+// 0x01 in bytes [0, k) (k <= 4 taken as 4): a v_dot4_u32_u8 mask for the first k bytes
+__device__ __forceinline__ uint32_t pb_ones_below(uint32_t k)
+{
+    return k >= 4u ? 0x01010101u : 0x01010101u & ((1u << (8u * k)) - 1u);
+}
+
+// Sums of the bytes (y_t >> 16) & 0xFF of the first dn (<= 16) states of the walk y_0 = y,
+// y_(t+1) = a y_t + c (mod 2^24), split by the parity of t: returns the even-t sum, odd-t in *odd.
+// Sixteen v_mad_u32_u24 (per-lane a and c: the walk runs forward or backward), the bytes packed
+// four to a dword (pb_pack4) and summed under a prefix mask by v_dot4_u32_u8 (the former per-step
+// compare / select / add chains compiled into v_mad_u64_u32, a quarter-rate instruction, per step)
+__device__ __forceinline__ uint32_t pb_walk_sums(uint32_t y, uint32_t a, uint32_t c, uint32_t dn, uint32_t *odd)
+{
+    uint32_t x[16];
+    x[0] = y;
+#pragma unroll
+    for (int t = 1; t < 16; ++t)
+        x[t] = pb_mad24v(x[t - 1], a, c);
+    const uint32_t e0 = pb_pack4(x[0], x[2], x[4], x[6]), e1 = pb_pack4(x[8], x[10], x[12], x[14]);
+    const uint32_t o0 = pb_pack4(x[1], x[3], x[5], x[7]), o1 = pb_pack4(x[9], x[11], x[13], x[15]);
+    const uint32_t ne = (dn + 1u) >> 1, no = dn >> 1; // walked even / odd positions
+    const uint32_t se = __builtin_amdgcn_udot4(e1, pb_ones_below(ne > 4u ? ne - 4u : 0u),
+                                               __builtin_amdgcn_udot4(e0, pb_ones_below(ne), 0u, false), false);
+    *odd = __builtin_amdgcn_udot4(o1, pb_ones_below(no > 4u ? no - 4u : 0u),
+                                  __builtin_amdgcn_udot4(o0, pb_ones_below(no), 0u, false), false);
+    return se;
+}
+
 // Little-endian 16-bit word sum (mod 0xFFFF, in [1, 0xFFFF]) of the n >= 3 payload bytes drawn
 // from the LCG state st0 entering the payload (sequence.c:552-555), payload at an even L4 offset:
 // the value fold(sum of the bytes' words) takes (the orbit has no run of 3 zero bytes, so the true
-// sum is never 0).
+// sum is never 0).  Every multiply is a full-rate 24-bit one (the states are taken mod 2^24).
 __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0, uint32_t n)
 {
-    const uint32_t yp = (PB_A3 * st0 + PB_C3) & PB_M24; // the state of payload byte 0
+    const uint32_t yp = pb_mad24(st0, PB_A3 & PB_M24, pb_vgpr(PB_C3)) & PB_M24; // the state of payload byte 0
     uint32_t cur = 0, p = 0;
     // bits 0-11 one at a time; bits 12-23 in closed form: with N = M^4096 = (A, C), A = 1 + 2^14 u,
     // C = 2^12 v (v odd), N^j(x) = x + j ((A - 1) x + C) mod 2^24 (the dropped terms carry 2^26), so
@@ -2459,7 +2495,7 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     for (int i = 0; i < 12; ++i)
     {
         const uint32_t bit = 1u << i;
-        const uint32_t nx = __umul24(cur, pb_orb_a(i)) + pb_orb_c(i);
+        const uint32_t nx = pb_mad24(cur, pb_orb_a(i), pb_vgpr(pb_orb_c(i)));
         const bool take = ((cur ^ yp) & bit) != 0;
         cur = take ? nx : cur;
         p |= take ? bit : 0u;
@@ -2467,42 +2503,37 @@ __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0
     {
         constexpr uint32_t A12 = pb_orb_a(12), C12 = pb_orb_c(12);
         static_assert(((A12 - 1u) & 0x3FFFu) == 0u && (C12 & 0x1FFFu) == 0x1000u, "M^4096 shape");
-        const uint32_t w = (__umul24(yp & 0xFFFu, (A12 - 1u) >> 12) + (C12 >> 12)) & 0xFFFu;
+        const uint32_t w = pb_mad24(yp & 0xFFFu, (A12 - 1u) >> 12, pb_vgpr(C12 >> 12)) & 0xFFFu;
         uint32_t x = w; // w^-1 mod 2^12: correct to 3 bits, each Newton step doubles them
-        x = __umul24(x, (2u - __umul24(w, x)) & 0xFFFu) & 0xFFFu;
-        x = __umul24(x, (2u - __umul24(w, x)) & 0xFFFu) & 0xFFFu;
-        const uint32_t j = __umul24(((yp - cur) >> 12) & 0xFFFu, x) & 0xFFFu;
+        x = pb_mul24v(x, (2u - pb_mul24v(w, x)) & 0xFFFu) & 0xFFFu;
+        x = pb_mul24v(x, (2u - pb_mul24v(w, x)) & 0xFFFu) & 0xFFFu;
+        const uint32_t j = pb_mul24v(((yp - cur) >> 12) & 0xFFFu, x) & 0xFFFu;
         p |= j << 12;
     }
     const uint2 jq = K.jump[n - 1 + PB_JNEG]; // L^(3n): the state one past the payload
-    const uint32_t yq = jq.x * yp + jq.y;
+    const uint32_t yq = pb_mad24v(yp, jq.x, jq.y) & PB_M24;
     uint32_t q = p + n, wrap = 0;
     if (q >= (1u << 24)) // the run wraps the orbit (2^24 is even: parities keep)
         q -= 1u << 24, wrap = K.orbit_tot;
     // prefix sums at p and q from the nearer sampled position (floor or ceil, <= 16 steps): walk the
-    // bytes in between with M (forward, subtract) or M^-1 (backward, add); a[t & 1] collects the
-    // walked bytes of one parity, the first walked position having parity par
+    // bytes in between with M (forward, subtract) or M^-1 (backward, add); the walked bytes of
+    // each parity are summed, the first walked position having parity par
     constexpr uint32_t SM = (1u << PB_ORB_SH) - 1u, HALF = (SM + 1u) >> 1;
+    static_assert(HALF <= 16u, "pb_walk_sums walks at most 16 states");
     const bool fp = (p & SM) > HALF, fq = (q & SM) > HALF; // forward to the next sample
     const uint32_t ip = (p >> PB_ORB_SH) + (fp ? 1u : 0u), iq = (q >> PB_ORB_SH) + (fq ? 1u : 0u);
     const uint32_t tp = K.orbit[ip], tq = K.orbit[iq];
     const uint32_t dp = fp ? SM + 1u - (p & SM) : (p & SM), dq = fq ? SM + 1u - (q & SM) : (q & SM);
     const uint32_t ap_ = fp ? PB_A3 & PB_M24 : PB_A3I, cp_ = fp ? PB_C3 & PB_M24 : PB_C3I;
     const uint32_t aq_ = fq ? PB_A3 & PB_M24 : PB_A3I, cq_ = fq ? PB_C3 & PB_M24 : PB_C3I;
-    uint32_t y = fp ? yp : __umul24(yp, PB_A3I) + PB_C3I; // backward: from position p - 1
-    uint32_t z = fq ? yq : __umul24(yq, PB_A3I) + PB_C3I;
-    uint32_t ap[2] = {0u, 0u}, aq[2] = {0u, 0u};
-#pragma unroll
-    for (uint32_t t = 0; t < HALF; ++t)
-    {
-        ap[t & 1u] += t < dp ? (y >> 16) & 0xFFu : 0u;
-        aq[t & 1u] += t < dq ? (z >> 16) & 0xFFu : 0u;
-        y = __umul24(y, ap_) + cp_;
-        z = __umul24(z, aq_) + cq_;
-    }
+    const uint32_t y = fp ? yp : pb_mad24v(yp, pb_vgpr(PB_A3I), pb_vgpr(PB_C3I)); // backward: from position p - 1
+    const uint32_t z = fq ? yq : pb_mad24v(yq, pb_vgpr(PB_A3I), pb_vgpr(PB_C3I));
+    uint32_t ap1, aq1;
+    const uint32_t ap0 = pb_walk_sums(y, ap_, cp_, dp, &ap1);
+    const uint32_t aq0 = pb_walk_sums(z, aq_, cq_, dq, &aq1);
     // even / odd position sums of the walked bytes (the first walked position: p, or p - 1)
     const uint32_t pp = fp ? p & 1u : (p & 1u) ^ 1u, pq = fq ? q & 1u : (q & 1u) ^ 1u;
-    const uint32_t sEp = ap[pp], sOp = ap[pp ^ 1u], sEq = aq[pq], sOq = aq[pq ^ 1u];
+    const uint32_t sEp = pp ? ap1 : ap0, sOp = pp ? ap0 : ap1, sEq = pq ? aq1 : aq0, sOq = pq ? aq0 : aq1;
     // PE / PO at p and q, each in [0, 2 * 0xFFFF)
     const uint32_t PEp = fp ? (tp & 0xFFFFu) + 0xFFFFu - sEp : (tp & 0xFFFFu) + sEp;
     const uint32_t POp = fp ? (tp >> 16) + 0xFFFFu - sOp : (tp >> 16) + sOp;
@@ -2961,7 +2992,7 @@ __global__ __launch_bounds__(256) void pb_scatter_fixed(const uint8_t *src, uint
 
 // write-only roofline probe: each workgroup streams PER contiguous 4-KiB sweeps
 // of 16-B stores (PER = 4: the linear build kernels' shape; PER = 1: 4 KiB per
-// workgroup, the fastest plain fill measured, tools/wbench.hip)
+// workgroup, the fastest plain fill measured, probes/wbench.hip)
 template <bool NT, int PER, bool XR = false> // XR: XCD-contiguous regions (pb_xcd_region)
 __global__ __launch_bounds__(256) void pb_fill_kernel(pb_u32x4 *dst, uint64_t n16, uint32_t v)
 {
@@ -3409,7 +3440,7 @@ __global__ __launch_bounds__(512) void pb_fill512_kernel(pb_u32x4 *dst, uint64_t
         dst[c] = pb_u32x4{v, v ^ (uint32_t)c, v, (uint32_t)c};
 }
 
-// Write-roofline probe shapes (tools/wbench.hip, profiles/r02/wbench: the fastest plain
+// Write-roofline probe shapes (probes/wbench.hip, profiles/r02/wbench: the fastest plain
 // fills found; dynamic LDS caps the workgroups per CU, and fewer concurrent writers
 // write faster down to 4 per CU):
 //  0  16 KiB per workgroup, 4 plain 16-B stores per lane     4  4 KiB, LDS-capped at 5 workgroups / CU

@@ -12,8 +12,8 @@
 //     page walkers vs region writers), and frame buffers built from physical chunks
 //     (pr_frames_vmm: hipMemCreate chunks mapped in order or shuffled).
 // Built by scripts/r05/build_probe.sh into lib/libpbprobe.so; driven by scripts/r05/probe.py.
-#include "../csrc/pbgpu_kernels.hip"
-#include "../csrc/pbgpu.cpp"
+#include "../pb-af-xdp_amd/csrc/pbgpu_kernels.hip"
+#include "../pb-af-xdp_amd/csrc/pbgpu.cpp"
 
 namespace
 {

@@ -1,4 +1,4 @@
-"""Round-5 A/B probe driver (lib/libpbprobe.so from tools/r05_probe.hip; tool only).
+"""Round-5 A/B probe driver (lib/libpbprobe.so from probes/r05_probe.hip; tool only).
 
 python3 scripts/r05/probe.py MODE [reps]
 (the pb_fpage_kernel modes "fpage" / "fpord" are in commit 37dc421 with the kernel)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Write-roofline shape search + address-map probes (tools/wbench.hip), round 2.
+# Write-roofline shape search + address-map probes (probes/wbench.hip), round 2.
 # One file per section under gpurun_out/wbench/ (committed as profiles/r02/wbench/).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/wbench
