@@ -167,7 +167,29 @@ struct pb_kargs
     uint32_t img_np;
     pb_div img_div;         // division by img_np
     uint32_t img_solo;      // 1: single builds too (PBGPU_XP_IMG=2); else only pb_batch_kernel's part
+    // pb_orbit_sum (pb_vline_kernel, pb_vrec_kernel): the discrete log mod 2^12 by table, entry
+    // y mod 2^12 = p | (M^p(0) mod 2^24 >> 12) << 12, p = the position of y on M's orbit mod 2^12
+    const uint32_t *dlog12;
+    // packed variable lengths as XCD-owned 4-KiB pages (pb_vrec_kernel + pb_vpage_kernel, DESIGN.md
+    // 5.5): per frame {seed, L4 checksum | length << 16}; per page {the frame holding its first
+    // byte, that frame's start - the page's start}
+    uint32_t vp;            // 1: launch them instead of pb_vline_kernel
+    uint32_t vp_nfp;        // frame slots per page (the most frames touching one page, <= 64)
+    uint32_t vp_grid;       // page-kernel workgroups (4 pages each): the launch's longest possible stream
+    uint2 *vp_rec;
+    uint2 *vp_pt;
+    const uint2 *lcg48i;    // lcg48i[c] = L^(-48 c), c < PB_VP_NCI
+    const uint4 *m16;       // chunk byte masks by plo + phi (PB_VL_NMASK rows: bytes [plo, phi))
+    uint32_t vp_wgt;        // pb_vpage_kernel's threads per workgroup: 256 (4 pages) or 512 (8)
 };
+// pb_vpage_kernel: page-relative byte u = start - page start + PB_VP_BIAS (frames < 4 KiB start
+// after the previous page's start), 16-B chunk indices u >> 4 < PB_VP_NCI
+#define PB_VP_BIAS 4096u
+#define PB_VP_NCI 512u
+// its LDS: 33 chunk masks and a count record per wave, then per wave nfp 16-B records,
+// nfp * nsp + 1 header chunks and 256 chunk marks
+#define PB_VP_WAVE_LDS(nfp, nsp) ((size_t)(nfp) * 16 * (1 + (size_t)(nsp)) + 16 + 256)
+#define PB_VP_LDS(nfp, nsp, nw) ((size_t)PB_VL_NMASK * 16 + 8 * (size_t)(nw) + (nw) * PB_VP_WAVE_LDS(nfp, nsp))
 // pb_fstage_kernel's LDS besides the stage: header image (16 dwords) + z, checksum start per frame
 #define PB_FST_LDS(wgf) ((size_t)(wgf) * (16 + 2) * 4)
 // pb_vstage_kernel's LDS besides the stage: lcg48 entries, header image + start, length, z, header

@@ -84,6 +84,7 @@ enum pb_kern_force
     PBO_K_VSTAGE, // =vstage: pb_vstage_kernel for packed variable lengths
     PBO_K_NOPAGE, // =nopage: no pb_xpage_kernel (linear small kernel)
     PBO_K_LINEAR, // =linear: neither page kernel
+    PBO_K_VPAGE,  // =vpage: the page-shaped packed writer (pb_vrec_kernel + pb_vpage_kernel)
 };
 
 struct pb_opts
@@ -115,6 +116,9 @@ struct pb_opts
     bool umem_dma = false;   // PBGPU_UMEM_DMA=1: land through DMA copies, not the mapped scatter
     bool alloc_vmm = true;   // PBGPU_ALLOC=malloc: frame buffers from hipMalloc (fb_alloc)
     uint32_t alloc_chunk_mb = 64; // PBGPU_ALLOC_CHUNK_MB: fb_alloc's physical chunk
+    uint32_t vp_wgt = 0;       // PBGPU_VP_WGT=512: pb_vpage_kernel with 8 pages per workgroup
+    uint32_t vp_pages_pct = 0; // PBGPU_VP_PAGES_PCT: pb_vpage_kernel's grid as a percentage of the
+                               // expected pages (tests: a short grid, so waves take several pages)
 };
 
 uint32_t opt_u32(const char *name)
@@ -139,6 +143,7 @@ pb_opts read_opts()
                    : !strcmp(k, "vstage") ? PBO_K_VSTAGE
                    : !strcmp(k, "nopage") ? PBO_K_NOPAGE
                    : !strcmp(k, "linear") ? PBO_K_LINEAR
+                   : !strcmp(k, "vpage") ? PBO_K_VPAGE
                                           : PBO_K_AUTO;
     o.g = opt_u32("PBGPU_G");
     if (o.g != 8 && o.g != 16 && o.g != 32 && o.g != 64)
@@ -169,6 +174,8 @@ pb_opts read_opts()
     o.land_spin = !opt_is("PBGPU_LAND_SPIN", "0");
     o.umem_dma = getenv("PBGPU_UMEM_DMA") != NULL;
     o.alloc_vmm = !opt_is("PBGPU_ALLOC", "malloc");
+    o.vp_pages_pct = opt_u32("PBGPU_VP_PAGES_PCT");
+    o.vp_wgt = opt_u32("PBGPU_VP_WGT") == 512 ? 512u : 256u;
     if (opt_u32("PBGPU_ALLOC_CHUNK_MB"))
         o.alloc_chunk_mb = opt_u32("PBGPU_ALLOC_CHUNK_MB");
     return o;
@@ -236,6 +243,9 @@ struct frames_events
     // on first use (packed32 set until then)
     uint32_t *d_off32 = nullptr;
     unsigned long long *d_rstart = nullptr;
+    // pb_vrec_kernel's records and page table (pb_vpage_kernel), allocated on first use
+    uint2 *d_vrec = nullptr;
+    uint2 *d_vpt = nullptr;
     bool packed32 = false;
     uint32_t wf = 0;
 };
@@ -259,6 +269,9 @@ struct pbgpu_ctx
     uint2 *d_jump = nullptr;
     uint2 *d_lcg48 = nullptr;
     uint32_t *d_orbit = nullptr; // pb_vline_kernel: LCG-orbit prefix sums (built on first use, 2 MiB)
+    uint32_t *d_dlog12 = nullptr; // pb_orbit_sum's discrete log mod 2^12 (16 KiB)
+    uint2 *d_lcg48i = nullptr;    // pb_vpage_kernel: L^(-48 c), c < PB_VP_NCI
+    uint4 *d_m16 = nullptr;       // pb_vpage_kernel: chunk byte masks by plo + phi
     uint32_t orbit_tot = 0;
     unsigned long long *d_counters = nullptr; // [PB_MAX_SEQUENCES][PB_CTR_SHARDS][PB_CTR_STRIDE]
     // the shard sums {frames, bytes} per sequence, written by pb_ctr_read into mapped pinned host
@@ -672,7 +685,51 @@ int pbgpu_open(int device, pbgpu_ctx **out)
             C = A16 * C + C16;
         }
     }
+    // L^(-48 c) (pb_vpage_kernel) and the discrete log of M = L^3 mod 2^12 (pb_orbit_sum)
+    std::vector<uint2> l48i(PB_VP_NCI);
+    std::vector<uint32_t> dlog12(4096);
+    std::vector<uint4> m16(PB_VL_NMASK);
+    for (int j = 0; j < PB_VL_NMASK; ++j) // bytes [lo, hi) of a 16-B chunk: j = lo + hi
+    {
+        const int lo = j > 16 ? j - 16 : 0, hi = j > 16 ? 16 : j;
+        uint32_t w[4];
+        for (int t = 0; t < 4; ++t)
+        {
+            w[t] = 0;
+            for (int b = 0; b < 4; ++b)
+                if (4 * t + b >= lo && 4 * t + b < hi)
+                    w[t] |= 0xFFu << (8 * b);
+        }
+        m16[j] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    {
+        uint32_t ai = PB_LCG_A; // PB_LCG_A^-1 mod 2^32 (Newton)
+        for (int i = 0; i < 5; ++i)
+            ai *= 2u - PB_LCG_A * ai;
+        const uint32_t ci = 0u - ai * PB_LCG_C; // L^-1(x) = ai x + ci
+        uint32_t A48 = 1, C48 = 0;
+        for (int i = 0; i < 48; ++i)
+            C48 = ai * C48 + ci, A48 = ai * A48;
+        uint32_t A = 1, C = 0;
+        for (uint32_t m = 0; m < PB_VP_NCI; ++m)
+        {
+            l48i[m] = make_uint2(A, C);
+            A = A48 * A;
+            C = A48 * C + C48;
+        }
+        const uint32_t a3 = (PB_LCG_A * PB_LCG_A * PB_LCG_A) & 0xFFFFFFu;
+        const uint32_t c3 = (PB_LCG_C * (PB_LCG_A * PB_LCG_A + PB_LCG_A + 1u)) & 0xFFFFFFu;
+        uint32_t x = 0;
+        for (uint32_t j = 0; j < 4096; ++j)
+        {
+            dlog12[x & 0xFFFu] = j | (x & 0xFFF000u);
+            x = (a3 * x + c3) & 0xFFFFFFu;
+        }
+    }
     if (upload(&ctx->d_jump, jt.data(), jt.size()) != PBGPU_OK || upload(&ctx->d_lcg48, l48.data(), l48.size()) != PBGPU_OK ||
+        upload(&ctx->d_lcg48i, l48i.data(), l48i.size()) != PBGPU_OK ||
+        upload(&ctx->d_dlog12, dlog12.data(), dlog12.size()) != PBGPU_OK ||
+        upload(&ctx->d_m16, m16.data(), m16.size()) != PBGPU_OK ||
         hipMalloc((void **)&ctx->d_counters, PB_CTR_BYTES) != hipSuccess ||
         hipMemset(ctx->d_counters, 0, PB_CTR_BYTES) != hipSuccess ||
         hipHostMalloc((void **)&ctx->h_ctr_sum, 2 * sizeof(unsigned long long) * PB_MAX_SEQUENCES,
@@ -724,6 +781,12 @@ void pbgpu_close(pbgpu_ctx *ctx)
         (void)hipFree(ctx->d_lcg48);
     if (ctx->d_orbit)
         (void)hipFree(ctx->d_orbit);
+    if (ctx->d_dlog12)
+        (void)hipFree(ctx->d_dlog12);
+    if (ctx->d_lcg48i)
+        (void)hipFree(ctx->d_lcg48i);
+    if (ctx->d_m16)
+        (void)hipFree(ctx->d_m16);
     if (ctx->d_counters)
         (void)hipFree(ctx->d_counters);
     if (ctx->h_ctr_sum)
@@ -1287,6 +1350,19 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                 K.vl_wgf = wf;
                 K.vl_nl48 = nl48;
                 K.vl_nlines = nlines;
+                // PBGPU_KERNEL=vpage, one payload: the page-shaped writer (pb_vrec_kernel +
+                // pb_vpage_kernel).  Bit-exact and immune to the buffer placement
+                // that slows pb_vline_kernel, but 7.1 vs 4.2 ms per 2^25 configs[2] frames: each
+                // page's frame setup runs one lane per frame (~6 of 64 lanes), 3.4 G VALU
+                // instructions per launch against 2.0 G (profiles/r06/vpage/)
+                const uint32_t nfp = (4096 + minf - 1) / minf + 1;
+                if (pls.size() == 1 && nfp <= 64 && O.kernel == PBO_K_VPAGE)
+                {
+                    K.vl = 0;
+                    K.vp = 1;
+                    K.vp_nfp = nfp;
+                    K.vp_wgt = O.vp_wgt;
+                }
             }
             if (fst_ok)
             {
@@ -1334,6 +1410,9 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
     K.blob = S.d_blob;
     K.jump = ctx->d_jump;
     K.lcg48 = ctx->d_lcg48;
+    K.lcg48i = ctx->d_lcg48i;
+    K.m16 = ctx->d_m16;
+    K.dlog12 = ctx->d_dlog12;
     K.counters = ctx->d_counters + PB_CTR_WORDS * seq_idx;
     // pb_ximg_kernel (static-payload ICMP frames): only IPv4 ID, TTL, checksum and
     // source address vary per frame, so the stream's bytes repeat every img_np = flen / gcd(flen,
@@ -1578,6 +1657,10 @@ void pbgpu_frames_free(pbgpu_ctx *ctx, pbgpu_frames *f)
             fb_free(fe->d_off32);
         if (fe->d_rstart)
             (void)hipFree(fe->d_rstart);
+        if (fe->d_vrec)
+            fb_free(fe->d_vrec);
+        if (fe->d_vpt)
+            (void)hipFree(fe->d_vpt);
         if (fe->landed)
             (void)hipEventDestroy(fe->landed);
         delete fe;
@@ -1748,8 +1831,8 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
         K.vblk_sum = nullptr;
         K.vblk_l2 = nullptr;
         K.offsets_w = nullptr;
-        const uint32_t wgf = K.vl ? K.vl_wgf : K.stage_wgf;
-        if (K.vl || (K.vst && K.stage_wgf >= PB_VST_SCAN_MIN_WGF && !S.opt.vst_scan3))
+        const uint32_t wgf = K.vp ? (uint32_t)PB_WG : (K.vl ? K.vl_wgf : K.stage_wgf);
+        if (K.vl || K.vp || (K.vst && K.stage_wgf >= PB_VST_SCAN_MIN_WGF && !S.opt.vst_scan3))
         {
             // pb_vline_kernel / pb_vstage_kernel: per-workgroup length sums, their scan, offsets
             // written by the build
@@ -1762,7 +1845,31 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
             K.vblk_sum = bsum;
             K.vblk_l2 = l2;
             K.offsets_w = out->offsets;
-            if (K.vl)
+            if (K.vp)
+            {
+                // the record pass's records (8 B per frame) and page table (8 B per page of the
+                // buffer's capacity); the page grid covers the longest stream these frames can make
+                if (fe->d_vrec == nullptr)
+                    HIPCHK(fb_alloc(ctx, (void **)&fe->d_vrec, out->capacity_frames * sizeof(uint2)));
+                if (fe->d_vpt == nullptr)
+                    HIPCHK(hipMalloc((void **)&fe->d_vpt, (out->capacity_bytes / 4096 + 2) * sizeof(uint2)));
+                K.vp_rec = fe->d_vrec;
+                K.vp_pt = fe->d_vpt;
+                // the grid covers the expected stream (one random payload of uniform length: the
+                // mean frame) plus 1% and 64 pages; a longer stream is built by the same waves in
+                // later rounds.  (A grid for the longest possible stream, 1.87x configs[2]'s, spent
+                // ~2 ms per 2^25 frames on workgroups past the stream's end.)
+                const uint64_t pages_max = (nf * S.max_flen + 4095) / 4096;
+                uint64_t pages_est = (uint64_t)((double)nf * 0.5 * (S.min_flen + S.max_flen) * 1.01 / 4096.0) + 64;
+                if (S.opt.vp_pages_pct)
+                    pages_est = pages_est * S.opt.vp_pages_pct / 100 + 1;
+                const uint64_t pages = pages_est < pages_max ? pages_est : pages_max;
+                const uint64_t ppg = 8ull * (K.vp_wgt == 512 ? 8u : 4u); // pages per group of 8 workgroups
+                if ((pages + ppg - 1) / ppg * 8 > 0x7FFFFFFFull)
+                    return PBGPU_ENOSPC;
+                K.vp_grid = (uint32_t)((pages + ppg - 1) / ppg * 8);
+            }
+            if (K.vl || K.vp)
             {
                 // 4 B per frame and 8 B per region instead of 8 B per frame
                 // (each checked on its own: a failed second allocation must not leave the pair
@@ -2599,7 +2706,10 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
     if (!S.loaded)
         return PBGPU_ENOENT;
     const pb_kargs &K = S.K;
-    if (K.vl)
+    if (K.vp)
+        snprintf(buf, n, "pb_vpage_kernel<%u, %u> (after pb_vrec_kernel<%u, %u>)", K.hl,
+                 (K.flags & PBK_L4_CSUM) ? 1u : 0u, K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
+    else if (K.vl)
         snprintf(buf, n, "pb_vline_kernel<%u, %u>", K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
     else if (K.fst_g)
         snprintf(buf, n, "pb_fstage_kernel<%u, %u>", K.fst_g, (K.flags & PBK_L4_CSUM) ? 1u : 0u);

@@ -2487,19 +2487,15 @@ __device__ __forceinline__ uint32_t pb_walk_sums(uint32_t y, uint32_t a, uint32_
 __device__ __forceinline__ uint32_t pb_orbit_sum(const pb_kargs &K, uint32_t st0, uint32_t n)
 {
     const uint32_t yp = pb_mad24(st0, PB_A3 & PB_M24, pb_vgpr(PB_C3)) & PB_M24; // the state of payload byte 0
-    uint32_t cur = 0, p = 0;
-    // bits 0-11 one at a time; bits 12-23 in closed form: with N = M^4096 = (A, C), A = 1 + 2^14 u,
-    // C = 2^12 v (v odd), N^j(x) = x + j ((A - 1) x + C) mod 2^24 (the dropped terms carry 2^26), so
-    // j = ((yp - cur) >> 12) / (((A - 1) >> 12) yp + v) mod 2^12 (the divisor is odd)
-#pragma unroll
-    for (int i = 0; i < 12; ++i)
-    {
-        const uint32_t bit = 1u << i;
-        const uint32_t nx = pb_mad24(cur, pb_orb_a(i), pb_vgpr(pb_orb_c(i)));
-        const bool take = ((cur ^ yp) & bit) != 0;
-        cur = take ? nx : cur;
-        p |= take ? bit : 0u;
-    }
+    // bits 0-11 by table (K.dlog12: M mod 2^12 walks all 4096 residues from 0, so the position mod
+    // 2^12 and the state there, cur = M^p(0) mod 2^24 whose low 12 bits are yp's, depend on yp mod
+    // 2^12 alone; the former 12 conditional steps cost ~70 VALU per frame); bits 12-23 in closed
+    // form: with N = M^4096 = (A, C), A = 1 + 2^14 u, C = 2^12 v (v odd), N^j(x) = x + j ((A - 1) x + C)
+    // mod 2^24 (the dropped terms carry 2^26), so j = ((yp - cur) >> 12) / (((A - 1) >> 12) yp + v)
+    // mod 2^12 (the divisor is odd)
+    const uint32_t e12 = K.dlog12[yp & 0xFFFu];
+    uint32_t p = e12 & 0xFFFu;
+    const uint32_t cur = (e12 & 0xFFF000u) | (yp & 0xFFFu);
     {
         constexpr uint32_t A12 = pb_orb_a(12), C12 = pb_orb_c(12);
         static_assert(((A12 - 1u) & 0x3FFFu) == 0u && (C12 & 0x1FFFu) == 0x1000u, "M^4096 shape");
@@ -2807,6 +2803,279 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
     }
     if (tid == 0) // the workgroup stores exactly [lo, hi) (the launch's last chunk zero-padded)
         pb_count(K, bxr, nown, hi_abs - lo_abs);
+}
+
+// ---------------- packed variable lengths as XCD-owned 4-KiB pages: pb_vrec_kernel + pb_vpage_kernel ----------------
+//
+// configs[2] in the page kernels' store shape: workgroup b's wave w owns page
+// ((b / 8) 4 + w) 8 + b % 8 of the packed stream, so every XCD writes one residue class of pages
+// inside one moving window and each wave retires after one page: the only store shape measured
+// immune to the buffer placement that slows the region writers (pb_vline_kernel 4.9 vs 4.2 ms).
+// A page finds its frames through two arrays written by the record pass, one lane per frame:
+//   rec[f] = {seed, L4 checksum | length << 16}   (8 B per frame; the L4 sum by pb_orbit_sum)
+//   pt[c]  = {the frame holding page c's first byte, its start - 4096 c}
+// so the page kernel's per-frame work is the header image from the seed and a length scan.
+
+// inclusive add scan over the wave's 64 lanes (DPP: row shifts, then row broadcasts)
+__device__ __forceinline__ uint32_t pb_wave_scan(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true); // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true); // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true); // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true); // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// Record pass: workgroup b takes frames [256 b, 256 b + 256) (the length pass ran at 256 frames per
+// workgroup), one lane per frame: seed -> r0 -> length, header fields and the L4 checksum
+// (sequence.c:434-594, as pb_vline_kernel's prologue), the start from the group sums and a
+// workgroup scan; writes the frame's 4-B offset, rec[f] and, if the frame holds a page's first byte,
+// pt[page].  The block sums' loads are issued first and read last.
+template <int HL, bool L4>
+__global__ __launch_bounds__(PB_WG) void pb_vrec_kernel(pb_kargs K)
+{
+    __shared__ uint32_t s_wsum[PB_WG / 64];
+    __shared__ unsigned long long s_part;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint64_t f = (uint64_t)b * PB_WG + tid;
+    const bool valid = f < K.n_frames;
+    // the group sums before this workgroup's (PB_VL_GRP workgroups per group)
+    unsigned long long part = 0;
+    if (wv == 0 && lane < (b & (PB_VL_GRP - 1u)))
+        part = K.vblk_sum[(b & ~(PB_VL_GRP - 1u)) + lane];
+    const unsigned long long base_l2 = K.vblk_l2[b / PB_VL_GRP];
+    uint32_t flen = 0, s = 0, csum = 0;
+    if (valid)
+    {
+        s = pb_seed(K.seed_base, K.seq, K.first_iter + f);
+        const uint32_t r0 = pb_rand_r(s);
+        const pb_frame_pl P = pb_payload_of(K.pl0, s, K.flags);
+        flen = HL + P.plen;
+        if (L4)
+        {
+            uint32_t d[16];
+            const uint2 rg1 = (K.flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
+            const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
+            uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) + pb_halves(d[12]) +
+                          pb_halves(d[13]);
+            if (K.flags & PBK_PSEUDO)
+                hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
+            const uint32_t ps = pb_orbit_sum(K, P.st0, P.plen);
+            csum = (~pb_fold(pb_fold(hs) + ps)) & 0xFFFFu;
+        }
+    }
+    const uint32_t inc = pb_wave_scan(flen);
+    if (wv == 0)
+    {
+#pragma unroll
+        for (uint32_t dd = 32; dd > 0; dd >>= 1)
+            part += __shfl_xor(part, dd, 64);
+        if (lane == 0)
+            s_part = part;
+    }
+    if (lane == 63u)
+        s_wsum[wv] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < PB_WG / 64; ++w)
+        pre += w < wv ? s_wsum[w] : 0u;
+    const uint64_t start = base_l2 + s_part + pre + inc - flen;
+    if (valid)
+    {
+        K.offsets32[f] = (uint32_t)start;
+        if (tid == 0)
+            K.vl_rstart[b] = start;
+        K.vp_rec[f] = make_uint2(s, csum | (flen << 16));
+        const uint64_t pg = (start + 4095u) >> 12;
+        if ((pg << 12) < start + flen)
+            K.vp_pt[pg] = make_uint2((uint32_t)f, (uint32_t)(start - (pg << 12)));
+    }
+}
+
+// Page kernel: wave w of workgroup b builds page c (above) of the stream whose length the length
+// pass's scan left in offsets_w[n_frames]:
+//  * its pt entry (a scalar load) and the records of up to 64 frames from there; a length scan
+//    gives each frame's page-relative start; the nf frames that start before the page's end are
+//    its slots (nf <= vp_nfp);
+//  * one lane per slot: r0 and the header image from the seed, the L4 checksum from the record,
+//    a 16-B record {first chunk, payload start, end, LCG state at page chunk 0} and the image
+//    shifted to the frame's byte offset (pb_vline_kernel's layout), and a mark at the first chunk
+//    whose first byte is the frame's;
+//  * lane l builds chunks l, l + 64, l + 128, l + 192 of the page: its frame is the count of marks
+//    at or below the chunk (ballot + mbcnt, no map), its LCG state L^(48 ci) of the frame's state
+//    at chunk 0 (per-lane constants), 16 payload bytes blended with the header image under the
+//    payload's byte mask; four 1-KiB store instructions (the stream's last chunk zero-padded).
+// Each workgroup's count record is {frames starting in its pages, their page bytes}; pages past the
+// stream (the grid covers the longest possible one) record zeros.
+template <int HL, bool L4, int WGT = PB_WG>
+__global__ __launch_bounds__(WGT) void pb_vpage_kernel(pb_kargs K)
+{
+    constexpr uint32_t NW = WGT / 64; // pages (waves) per workgroup
+    constexpr uint32_t NSP = (15 + HL + 15) / 16; // chunks a frame's header can touch
+    constexpr uint32_t NHW = (HL + 6) / 4;       // image dwords written (pb_vline_kernel)
+    static_assert(3 + NHW <= 4 * NSP, "image slot");
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    const uint32_t NFP = K.vp_nfp;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    pb_u32x4 *const s_m16 = reinterpret_cast<pb_u32x4 *>(s_dyn);
+    uint2 *const s_cnt = reinterpret_cast<uint2 *>(s_m16 + PB_VL_NMASK);
+    uint8_t *const wb = reinterpret_cast<uint8_t *>(s_cnt + NW) + wv * PB_VP_WAVE_LDS(NFP, NSP);
+    pb_u32x4 *const s_rec = reinterpret_cast<pb_u32x4 *>(wb);
+    pb_u32x4 *const s_img = s_rec + NFP;
+    uint32_t *const s_mark = reinterpret_cast<uint32_t *>(s_img + NFP * NSP + 1);
+
+    const uint32_t b = blockIdx.x;
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane(((b >> 3) * NW + wv) * 8u + (b & 7u));
+    // every load that does not wait for the page's records is issued here, together: the
+    // stream's length and the page's pt entry (scalar; the grid's pages all have an entry, pages
+    // past the stream a stale one that is not used), the lane's chunk states L^(48 ci),
+    // ci = PB_VP_BIAS / 16 + 64 i + lane, and three 16 / 16 / 32-entry maps held one per lane for
+    // the frames' states (read by lane shuffles): lanes 0-15 L^(3 (1 - s0 - HL)) (payload byte 0
+    // at chunk byte s0 + HL), 16-31 L^(-48 j), 32-63 L^(-768 h)
+    const uint64_t total = K.offsets_w[K.n_frames];
+    uint2 e = K.vp_pt[c0];
+    uint2 lc[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i)
+        lc[i] = K.lcg48[PB_VP_BIAS / 16u + 64u * i + lane];
+    const uint2 tm = lane < 16u ? K.jump[PB_JNEG - (lane + HL)] : K.lcg48i[lane < 32u ? lane - 16u : (lane - 32u) << 4];
+    const uint2 rg1 = (K.flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u); // one range: uniform
+    // chunk byte masks by plo + phi, from the context's table (every wave writes the same rows)
+    uint4 m16row = make_uint4(0u, 0u, 0u, 0u);
+    if (lane < PB_VL_NMASK)
+        m16row = K.m16[lane];
+    uint32_t frames = 0, bytes = 0;
+    // the grid is sized for the expected stream (pbgpu.cpp); a longer one is taken by later rounds
+    // of the same waves (their pages keep the XCD: the stride is a multiple of 8 pages)
+    for (uint64_t c = c0; (c << 12) < total; c += (uint64_t)NW * gridDim.x)
+    {
+        if (c != c0)
+        {
+            e = K.vp_pt[c];
+            // the previous page's LDS reads before this page's writes
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const uint64_t f = (uint64_t)e.x + lane;
+        const bool fv = f < K.n_frames;
+        const uint2 r = fv ? K.vp_rec[f] : make_uint2(0u, 0u);
+        const uint32_t fl = r.y >> 16;
+        const int32_t st = (int32_t)e.y + (int32_t)(pb_wave_scan(fl) - fl); // page-relative start
+        const bool inp = fv && st < 4096;
+        const uint32_t nf = (uint32_t)__popcll(__ballot(inp)); // slots 0 .. nf - 1
+        const int32_t end_last = __shfl(st + (int32_t)fl, (int)nf - 1, 64);
+        const uint32_t pbytes = (uint32_t)min(end_last, 4096);
+        bytes += pbytes;
+        frames += nf - ((int32_t)e.y < 0 ? 1u : 0u);
+        s_mark[lane] = 0u;
+        if (lane < PB_VL_NMASK)
+            s_m16[lane] = pb_u32x4{m16row.x, m16row.y, m16row.z, m16row.w};
+        // the frame's three state maps, read from the lanes holding them (every lane takes part:
+        // a shuffle reads no lane that is switched off)
+        const uint32_t u = (uint32_t)(st + (int32_t)PB_VP_BIAS);
+        const uint32_t s0 = u & 15u, cs = u >> 4;
+        const uint32_t l1 = s0 << 2, l2 = (16u + (cs & 15u)) << 2, l3 = (32u + ((cs >> 4) & 31u)) << 2;
+        const uint32_t m1a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l1, (int)tm.x);
+        const uint32_t m1c = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l1, (int)tm.y);
+        const uint32_t m2a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l2, (int)tm.x);
+        const uint32_t m2c = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l2, (int)tm.y);
+        const uint32_t m3a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l3, (int)tm.x);
+        const uint32_t m3c = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l3, (int)tm.y);
+        uint32_t k0 = 256u;
+        if (inp)
+        {
+            const uint32_t s = r.x;
+            const uint32_t r0 = pb_rand_r(s);
+            uint32_t d[16];
+            (void)pb_header(K, r0, fl - HL, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
+            // the LCG state at the frame's first chunk (payload byte j at chunk byte s0 + HL + j),
+            // taken back to page chunk 0 by L^(-48 cs) = L^(-48 (cs % 16)) L^(-768 (cs / 16))
+            const uint32_t z = pb_mad24v(pb_mad24v(pb_mad24v(s, m1a, m1c), m2a, m2c), m3a, m3c);
+            s_rec[lane] = pb_u32x4{cs, u + HL, u + fl, z};
+            const uint32_t q = s0 >> 2, sh = s0 & 3u;
+            uint32_t *const img32 = reinterpret_cast<uint32_t *>(s_img + lane * NSP) + q;
+#pragma unroll
+            for (uint32_t w = 0; w < NHW; ++w)
+            {
+                const uint32_t lo = w > 0 ? d[w - 1] : 0u, hi = d[w];
+                img32[w] = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
+            }
+            if (L4) // the L4 checksum's two bytes over the image's zeros (its position is the sequence's)
+            {
+                uint8_t *const cb = reinterpret_cast<uint8_t *>(s_img + lane * NSP) + s0 + 4u * K.csum_dw + 2u * K.csum_hi;
+                cb[0] = (uint8_t)r.y;
+                cb[1] = (uint8_t)(r.y >> 8);
+            }
+            k0 = st <= 0 ? 0u : ((uint32_t)st + 15u) >> 4;
+        }
+        if (lane == nf) // the chunk after the last slot's: no frame starts there
+            s_img[nf * NSP] = pb_u32x4{0u, 0u, 0u, 0u};
+        // the marks' zeroing before the marks (a wave's LDS operations complete in order)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (k0 < 256u) // chunk k's mark: byte k / 64 of dword k % 64
+            reinterpret_cast<uint8_t *>(s_mark)[((k0 & 63u) << 2) + (k0 >> 6)] = 1u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t mk = s_mark[lane];
+        const uint32_t nch = (pbytes + 15u) >> 4;
+        uint8_t *const gout = K.out + ((uint64_t)c << 12) + (lane << 4);
+        uint32_t pre = 0; // marks in the earlier 64-chunk quarters
+        pb_u32x4 v[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+        {
+            const uint64_t B = __ballot(((mk >> (8u * i)) & 0xFFu) != 0u);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
+            const uint32_t fi = pre + below + (uint32_t)((B >> lane) & 1u) - 1u;
+            pre += (uint32_t)__popcll(B);
+            const pb_u32x4 rc = s_rec[fi];
+            const uint32_t ci = PB_VP_BIAS / 16u + 64u * i + lane;
+            const uint32_t m = ci - rc[0]; // chunk index within frame fi
+            const uint32_t x = pb_mad24v(rc[3], lc[i].x, lc[i].y);
+            const int32_t pb = (int32_t)(ci << 4);
+            const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
+            const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
+            const pb_u32x4 h = s_img[fi * NSP + min(m, NSP)];
+            uint32_t o0, o1, o2, o3;
+            pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+            const pb_u32x4 mm = s_m16[plo + phi];
+            v[i] = pb_u32x4{(o0 & mm[0]) | (h[0] & ~mm[0]), (o1 & mm[1]) | (h[1] & ~mm[1]),
+                            (o2 & mm[2]) | (h[2] & ~mm[2]), (o3 & mm[3]) | (h[3] & ~mm[3])};
+        }
+        if (nch == 256u)
+        {
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i)
+                pb_st16_nt(gout + (i << 10), v[i]);
+        }
+        else
+        {
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i)
+                if (64u * i + lane < nch)
+                    pb_st16_nt(gout + (i << 10), v[i]);
+        }
+    }
+    if (lane == 0)
+        s_cnt[wv] = make_uint2(frames, bytes);
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        uint32_t fr = 0, by = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w)
+            fr += s_cnt[w].x, by += s_cnt[w].y;
+        pb_count_at(K, b, pb_xcd_region(b, gridDim.x), fr, by);
+    }
 }
 
 // ---------------- variable length: lengths -> offsets -> tile map ----------------
@@ -3168,6 +3437,8 @@ extern "C" uint32_t pbk_build_grid(const pb_kargs *K)
 {
     const uint64_t n = K->n_frames;
     uint64_t per = 0;
+    if (K->vp)
+        return K->vp_grid;
     if (K->vl)
         per = K->vl_wgf;
     else if (K->fst_g)
@@ -3185,7 +3456,37 @@ extern "C" uint32_t pbk_build_grid(const pb_kargs *K)
 
 extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
 {
-    if (K->vl)
+    if (K->vp)
+    {
+        // the record pass, then the pages (both are the build: one timed span)
+        const uint32_t rgrid = (uint32_t)((K->n_frames + PB_WG - 1) / PB_WG);
+        const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
+        const uint32_t nsp = K->hl == 54 ? 5u : 4u;
+        const uint32_t nw = K->vp_wgt == 512 ? 8u : 4u;
+        const size_t lds = PB_VP_LDS(K->vp_nfp, nsp, nw);
+#define PB_VP(HH, LL)                                                                                       \
+    do                                                                                                      \
+    {                                                                                                       \
+        hipLaunchKernelGGL((pb_vrec_kernel<HH, LL>), dim3(rgrid), dim3(PB_WG), 0, st, *K);                  \
+        if (nw == 8)                                                                                        \
+            hipLaunchKernelGGL((pb_vpage_kernel<HH, LL, 512>), dim3(K->vp_grid), dim3(512), lds, st, *K);   \
+        else                                                                                                \
+            hipLaunchKernelGGL((pb_vpage_kernel<HH, LL>), dim3(K->vp_grid), dim3(PB_WG), lds, st, *K);      \
+    } while (0)
+        if (K->hl == 54)
+        {
+            if (l4)
+                PB_VP(54, true);
+            else
+                PB_VP(54, false);
+        }
+        else if (l4)
+            PB_VP(42, true);
+        else
+            PB_VP(42, false);
+#undef PB_VP
+    }
+    else if (K->vl)
     {
         const uint32_t grid = (uint32_t)((K->n_frames + K->vl_wgf - 1) / K->vl_wgf);
         const size_t lds = PB_VL_LDS(K->vl_wgf, K->hl == 54 ? 5 : 4, K->vl_nl48, K->vl_nlines) + K->lds_pad;

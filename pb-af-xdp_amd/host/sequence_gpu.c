@@ -282,6 +282,34 @@ static void tx_sink(void *ctx, const uint8_t *frame, uint32_t len, uint64_t addr
                 strerror(errno));
 }
 
+/* The reference's per-packet verbose line (sequence.c:612-631), from a frame as it sits in its
+ * UMEM slot: "[seq][payload] Sent <len> bytes of data from <src>:<sport> to <dst>:<dport>."
+ * The source is the configured src_ip string, else the frame's drawn source address (rand_ip's
+ * dotted string); the ports are the UDP / TCP header's (0 for ICMP), the destination the
+ * configured dst_ip string. */
+static void print_sent(int seq_num, uint32_t pl_idx, const pb_sequence_t *seq, const uint8_t *fr, uint16_t len)
+{
+    char sip[16];
+    const char *src = seq->ip.src_ip;
+    uint32_t sport = 0, dport = 0;
+    if (len >= 34)
+    {
+        if (src == NULL)
+        {
+            snprintf(sip, sizeof sip, "%u.%u.%u.%u", fr[26], fr[27], fr[28], fr[29]);
+            src = sip;
+        }
+        const uint32_t l4 = 14u + 4u * (fr[14] & 0xFu);
+        if ((fr[23] == 17 || fr[23] == 6) && l4 + 4u <= len)
+        {
+            sport = ((uint32_t)fr[l4] << 8) | fr[l4 + 1];
+            dport = ((uint32_t)fr[l4 + 2] << 8) | fr[l4 + 3];
+        }
+    }
+    fprintf(stdout, "[%d][%u] Sent %u bytes of data from %s:%u to %s:%u.\n", seq_num, pl_idx + 1, (unsigned)len,
+            src ? src : "", sport, seq->ip.dst_ip ? seq->ip.dst_ip : "", dport);
+}
+
 static void *gpu_worker(void *p)
 {
     worker_arg_t *w = (worker_arg_t *)p;
@@ -577,6 +605,7 @@ static void *gpu_worker(void *p)
             }
             else
                 __atomic_add_fetch(&total_bytes[w->seq_idx], bytes, __ATOMIC_RELAXED);
+            const uint32_t sent_slot = xsk.next_slot;
             if ((rc = pb_xsk_send(&xsk, ln, n)) != 0)
             {
                 fprintf(stderr, "[%d][%d] ERROR - Could not send packet on AF_XDP socket (%d) :: %s.\n", seq_num, 1,
@@ -585,6 +614,10 @@ static void *gpu_worker(void *p)
                 done = 3;
                 break;
             }
+            if (verbose) /* the slots keep these frames until this thread lands into them again */
+                for (uint32_t i = 0; i < n; ++i)
+                    print_sent(seq_num, (uint32_t)((f0 + i) % fpi), seq, umem + (size_t)(sent_slot + i) * PB_FRAME_SIZE,
+                               ln[i]);
             __atomic_add_fetch(&total_pckts[w->seq_idx], n, __ATOMIC_RELAXED);
             my_frames += n;
             f0 += n;

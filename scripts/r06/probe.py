@@ -46,7 +46,7 @@ def emit(d):
 
 CAPS = {8: 0, 6: 27136, 5: 32768, 4: 40960, 3: 54272}
 
-if what == "gate":
+if what in ("gate", "shapes"):
     n = 1 << 25
     ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
     mf, mb = ctx.build_size(0, n)
@@ -70,6 +70,11 @@ if what == "gate":
     V = [("gate strided", 0)] + [(f"gate strided cap{c}", 0, CAPS[c]) for c in (6, 5, 4, 3)] + \
         [("gate contiguous", 1), ("gate contiguous cap4", 1, CAPS[4]), ("stores strided", 2),
          ("stores strided cap4", 2, CAPS[4]), ("stores contiguous", 3)]
+    if what == "shapes":
+        V = [("stores strided", 2), ("stores contiguous", 3), ("stores strided wg64", 4), ("stores contig wg64", 5),
+             ("stores strided wg128", 6), ("stores contig wg128", 7), ("stores strided wg512", 8),
+             ("stores contig wg512", 9), ("gate strided", 0), ("gate strided wg64", 10), ("gate strided wg128", 11),
+             ("gate strided wg512", 12)]
     fills = {"fill 4KiB/wg": 2, "fill 4KiB/wg XCD-contig": 10, "fill 4KiB/wg cap4": 5, "fill 208KiB region": 12}
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.6:  # clock ramp

@@ -1,0 +1,54 @@
+"""configs[2] kernels side by side in one process on the same buffers (tool only):
+python3 scripts/r06/vp_ab.py [reps] [nbuf] [variants...]
+variants: PBGPU_KERNEL values to load (default: "" = the library default, and "vline"); each is
+loaded into its own slot, then every buffer is built by every variant, reps rounds, 10 launches per
+timing (TIMING_LAUNCH medians).  One JSON line per (buffer, variant)."""
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pb-af-xdp_amd")]
+import pb_configs as pc  # noqa: E402
+from pbgpu import GpuContext, Sequence  # noqa: E402
+
+REPS = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+NBUF = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+VARS = sys.argv[3:] or ["", "vpage"]
+n = 1 << 25
+ctx = GpuContext(0)
+seq = Sequence.from_config(pc.get("c3_udp_var"))
+names = {}
+for i, v in enumerate(VARS):
+    # a variant is a PBGPU_KERNEL value, optionally with PBGPU_VP_WGT after a colon (vpage:512)
+    kern, _, wgt = v.partition(":")
+    for key, val in (("PBGPU_KERNEL", kern), ("PBGPU_VP_WGT", wgt)):
+        if val:
+            os.environ[key] = val
+        else:
+            os.environ.pop(key, None)
+    ctx.load_sequence(i, seq, pc.SEED_BASE)
+    names[i] = ctx.kernel_name(i)
+os.environ.pop("PBGPU_KERNEL", None)
+os.environ.pop("PBGPU_VP_WGT", None)
+bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(NBUF)]
+ctx.set_timing(ctx.TIMING_LAUNCH)
+t0 = time.perf_counter()
+while time.perf_counter() - t0 < float(os.environ.get("VP_RAMP", "0.6")):
+    ctx.build(0, 0, n, bufs[0])
+ctx.sync()
+ctx.kernel_times()
+res = {}
+for r in range(REPS):
+    for b, fb in enumerate(bufs):
+        for i in range(len(VARS)):
+            for k in range(int(os.environ.get("VP_LAUNCHES", "10"))):
+                ctx.build(i, k * n, n, fb)
+            ctx.sync()
+            t = ctx.kernel_times()
+            res.setdefault((b, i), []).append(float(statistics.median(t)))
+for (b, i), v in sorted(res.items()):
+    print(json.dumps({"buf": b, "variant": VARS[i] or "default", "kernel": names[i], "ms_med": round(statistics.median(v), 4),
+                      "ms_min": round(min(v), 4), "all": [round(x, 4) for x in v]}), flush=True)

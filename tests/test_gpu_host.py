@@ -146,3 +146,52 @@ def test_cli_null_tx_end_to_end(tmp_path):
     assert f"total of {n} packets and {64 * n} bytes" in r.stdout
     print(f"end-to-end (null TX ring, 64-B frames): {n / dt / 1e6:.1f} Mpps incl. process start")
     assert n / dt > 2e6  # sanity only: process start and GPU init are in dt (scripts/e2e_probe.py measures)
+
+
+def _sent_line(seq_num, pl_idx, frame, src_ip, dst_ip):
+    """The reference's verbose line for one sent frame (sequence.c:612-631), formatted from the
+    oracle's bytes: the configured source (or the frame's drawn one), the UDP / TCP ports."""
+    src = src_ip if src_ip else ".".join(str(b) for b in frame[26:30])
+    sport = dport = 0
+    if frame[23] in (6, 17):
+        l4 = 14 + 4 * (frame[14] & 15)
+        sport, dport = struct.unpack(">HH", frame[l4:l4 + 4])
+    return "[%d][%d] Sent %d bytes of data from %s:%d to %s:%d." % (seq_num, pl_idx + 1, len(frame), src, sport, dst_ip,
+                                                                     dport)
+
+
+@pytest.mark.parametrize("proto,extra,cfg_l4", [
+    ("udp", ["--udport", "27015", "--pmin", "0", "--pmax", "300"], {"udp": {"dport": 27015}}),
+    ("tcp", ["--tdport", "80", "--syn", "1", "--pmin", "6", "--pmax", "6"], {"tcp": {"dport": 80, "syn": 1}}),
+    ("icmp", ["--pmin", "10", "--pmax", "60"], {}),
+])
+def test_cli_verbose_sent_lines(tmp_path, proto, extra, cfg_l4):
+    """pcktbatch-gpu -v prints the reference's per-packet line for every frame it submits
+    (sequence.c:612-631; README.md:23 runs the demo with -v): the lines, in order, equal the
+    ones formatted from the oracle's frames, and the pcap holds those frames."""
+    pcap = tmp_path / "v.pcap"
+    n, seed = 700, 0xABCDE
+    cmd = [BIN, "-z", "-v", "--interface", "pbnodev0", "--smac", pc.SMAC, "--dmac", pc.DMAC, "--dip", pc.DIP,
+           "--sip", "10.30.0.0/16", "--protocol", proto] + extra + [
+           "--maxpckts", str(n), "--delay", "0", "--gpubatch", "256", "--seed", str(seed), "--pcap", str(pcap)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if " Sent " in ln]
+    cfg = {"eth": {"smac": pc.SMAC, "dmac": pc.DMAC}, "ip": {"dip": pc.DIP, "ranges": ["10.30.0.0/16"], "protocol": proto},
+           "payloads": [{"length": {"min": int(extra[extra.index("--pmin") + 1]),
+                                    "max": int(extra[extra.index("--pmax") + 1])}}]}
+    cfg.update(cfg_l4)
+    want = ob.frames(Sequence.from_config(cfg), 0, 0, n, seed)
+    assert read_pcap(pcap) == want
+    assert lines == [_sent_line(1, 0, f, None, pc.DIP) for f in want]
+
+
+def test_cli_verbose_static_source(tmp_path):
+    """With a static --sip the line names the configured source string (sequence.c:630)."""
+    cmd = [BIN, "-z", "-v", "--interface", "pbnodev0", "--smac", pc.SMAC, "--dmac", pc.DMAC, "--dip", pc.DIP,
+           "--sip", "192.168.9.9", "--protocol", "udp", "--usport", "4000", "--udport", "27015", "--pmin", "8",
+           "--pmax", "8", "--maxpckts", "50", "--delay", "0", "--gpubatch", "64", "--seed", "5"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if " Sent " in ln]
+    assert lines == ["[1][1] Sent 50 bytes of data from 192.168.9.9:4000 to %s:27015." % pc.DIP] * 50

@@ -20,12 +20,17 @@ SHAPES = [
     ("gpf", {"PBGPU_KERNEL": "gpf"}, ("pb_gpf_kernel", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("nopage_small", {"PBGPU_KERNEL": "nopage"},
      ("pb_small_kernel", "pb_xsmall_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel",
-      "pb_vline_kernel")),
+      "pb_vline_kernel", "pb_vpage_kernel")),
     ("xpage_forced", {"PBGPU_XP_FORCE": "1"},
      ("pb_xpage_kernel", "pb_xsmall_kernel", "pb_small_kernel<", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel",
-      "pb_vstage_kernel", "pb_vline_kernel")),
+      "pb_vstage_kernel", "pb_vline_kernel", "pb_vpage_kernel")),
     ("linear_small", {"PBGPU_KERNEL": "linear"},
-     ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel", "pb_vline_kernel")),
+     ("pb_small_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_fstage_kernel", "pb_vstage_kernel", "pb_vline_kernel",
+      "pb_vpage_kernel")),
+    # the page-shaped packed writer (pb_vrec_kernel + pb_vpage_kernel) on every config
+    ("vpage", {"PBGPU_KERNEL": "vpage"},
+     ("pb_vpage_kernel", "pb_vline_kernel", "pb_vstage_kernel", "pb_xsmall_kernel", "pb_xpage_kernel", "pb_small_kernel<",
+      "pb_fstage_kernel", "pb_stage_kernel", "pb_gpf_kernel", "pb_ximg_kernel")),
     ("stage_g8_wgf5", {"PBGPU_KERNEL": "stage", "PBGPU_G": "8", "PBGPU_WGF": "5"},
      ("pb_stage_kernel<8", "pb_xsmall_kernel", "pb_small_kernel<")),
     ("stage_g64_kb4", {"PBGPU_KERNEL": "stage", "PBGPU_G": "64", "PBGPU_STAGE_KB": "4"},
@@ -318,14 +323,19 @@ VL_RANGES = [(32, 33), (32, 40), (32, 200), (60, 1500), (64, 1500), (1400, 1500)
 @pytest.mark.parametrize("lo,hi", VL_RANGES)
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
 @pytest.mark.parametrize("csum", [True, False])
-def test_vline_variable_lengths(ctx, proto, lo, hi, csum):
+@pytest.mark.parametrize("kernel", ["vpage", "vline"])
+def test_vline_variable_lengths(ctx, monkeypatch, proto, lo, hi, csum, kernel):
+    """pb_vline_kernel (the default) and pb_vpage_kernel (PBGPU_KERNEL=vpage: up to 57 frames per
+    page at 74 B, frames up to 4 KiB starting up to a page before the page)."""
+    if kernel == "vpage":
+        monkeypatch.setenv("PBGPU_KERNEL", "vpage")
     hl = 54 if proto == "tcp" else 42
     cfg = _fst_cfg(proto, hl + 100, csum)
     cfg["payloads"] = [{"length": {"min": lo, "max": hi}}]
     big = max(300, min(40000, (24 << 20) // (hl + hi)))
     for first, n in ((5, 1), (0, 3), (11, 253), (2 ** 40 + 7, 1000), (1, big)):
         kern = _check(ctx, cfg, first, n)
-        assert kern.startswith("pb_vline_kernel<%d, %d>" % (hl, int(csum))), kern
+        assert kern.startswith("pb_%s_kernel<%d, %d>" % (kernel, hl, int(csum))), kern
 
 
 @pytest.mark.parametrize("wgf", ["32", "100", "252"])
@@ -347,46 +357,62 @@ def test_vline_offsets_across_4gib_boundaries(ctx, monkeypatch):
     be the oracle's bytes at the oracle's offsets."""
     seq = Sequence.from_config(pc.get("c3_udp_var"))
     n, first = 1 << 23, 12345
-    offs = {}
-    for kernel in ("vline", "vstage"):
-        if kernel == "vstage":
-            monkeypatch.setenv("PBGPU_KERNEL", "vstage")
+    offs, data = {}, {}
+    for kernel in ("vline", "vpage", "vstage"):
+        if kernel != "vline":
+            monkeypatch.setenv("PBGPU_KERNEL", kernel)
         ctx.load_sequence(6, seq, pc.SEED_BASE)
         fb = ctx.alloc_frames(*ctx.build_size(6, n))
         ctx.build(6, first, n, fb)
         ctx.sync()
         offs[kernel] = fb.offsets()
-        name = ctx.kernel_name(6)
-        if kernel == "vline":
-            assert name.startswith("pb_vline_kernel")
-            data = fb.packed()
-        else:
-            assert name.startswith("pb_vstage_kernel")
+        assert ctx.kernel_name(6).startswith("pb_%s_kernel" % kernel)
+        if kernel != "vstage":
+            data[kernel] = fb.packed()
         fb.free()
-    o = offs["vline"]
+    o = offs["vpage"]
     assert o[-1] > (1 << 32)  # the build crosses a 4-GiB boundary
-    assert np.array_equal(o, offs["vstage"])
+    assert np.array_equal(o, offs["vstage"]) and np.array_equal(o, offs["vline"])
+    assert np.array_equal(data["vpage"], data["vline"])
     for k in range(1, int(o[-1] >> 32) + 1):
         f = int(np.searchsorted(o, k << 32, side="right")) - 1  # the frame holding byte k * 2^32
         f0 = max(0, f - 16)
         od, oo = ob.build(seq, 6, first + f0, 32, pc.SEED_BASE)
         assert np.array_equal(o[f0:f0 + 33] - o[f0], oo), k
-        assert np.array_equal(data[int(o[f0]):int(o[f0 + 32])], od), k
+        assert np.array_equal(data["vpage"][int(o[f0]):int(o[f0 + 32])], od), k
 
 
 def test_vline_matches_vstage_at_size(ctx, monkeypatch):
-    """configs[2] at 2^22 frames: the two variable-length kernels build the same bytes."""
+    """configs[2] at 2^22 frames: the three variable-length kernels build the same bytes."""
     seq = Sequence.from_config(pc.get("c3_udp_var"))
     out = {}
-    for kernel in ("vline", "vstage"):
-        if kernel == "vstage":
-            monkeypatch.setenv("PBGPU_KERNEL", "vstage")
+    for kernel in ("vline", "vpage", "vstage"):
+        if kernel != "vline":
+            monkeypatch.setenv("PBGPU_KERNEL", kernel)
         ctx.load_sequence(6, seq, pc.SEED_BASE)
         fb = ctx.alloc_frames(*ctx.build_size(6, 1 << 22))
         ctx.build(6, 3 << 30, 1 << 22, fb)
         ctx.sync()
         out[kernel] = (fb.packed(), fb.offsets(), ctx.kernel_name(6))
         fb.free()
-    assert out["vline"][2].startswith("pb_vline_kernel") and out["vstage"][2].startswith("pb_vstage_kernel")
-    assert np.array_equal(out["vline"][1], out["vstage"][1])
-    assert np.array_equal(out["vline"][0], out["vstage"][0])
+    for kernel in out:
+        assert out[kernel][2].startswith("pb_%s_kernel" % kernel)
+    for kernel in ("vline", "vstage"):
+        assert np.array_equal(out["vpage"][1], out[kernel][1])
+        assert np.array_equal(out["vpage"][0], out[kernel][0])
+
+
+@pytest.mark.parametrize("pct", ["1", "30", "100"])
+@pytest.mark.parametrize("wgt", ["256", "512"])
+def test_vpage_short_grid_waves_take_several_pages(ctx, monkeypatch, pct, wgt):
+    """pb_vpage_kernel's grid covers the expected stream; a longer one is built by the same waves
+    in later rounds (PBGPU_VP_PAGES_PCT shrinks the grid so every wave loops), at 4 and 8 pages
+    per workgroup (PBGPU_VP_WGT): bit-exact."""
+    monkeypatch.setenv("PBGPU_KERNEL", "vpage")
+    monkeypatch.setenv("PBGPU_VP_PAGES_PCT", pct)
+    monkeypatch.setenv("PBGPU_VP_WGT", wgt)
+    for lo, hi in ((32, 33), (64, 1500), (3000, 4042)):
+        cfg = pc.get("c3_udp_var")
+        cfg["payloads"] = [{"length": {"min": lo, "max": hi}}]
+        kern = _check(ctx, cfg, 99, 30011)
+        assert kern.startswith("pb_vpage_kernel<"), kern

@@ -160,15 +160,19 @@ def test_sequence_streams_build_the_same_bytes(ctx):
             b.free()
 
 
-# pb_vline_kernel writes 4-B offsets and region starts; offsets[] is expanded on first use and
-# must follow every rebuild of the buffer (a stale expansion would keep the first build's)
-def test_packed_offsets_expand_after_every_build(ctx):
+# pb_vpage_kernel's record pass and pb_vline_kernel write 4-B offsets and region starts; offsets[]
+# is expanded on first use and must follow every rebuild of the buffer (a stale expansion would
+# keep the first build's)
+@pytest.mark.parametrize("kernel", ["vpage", "vline"])
+def test_packed_offsets_expand_after_every_build(ctx, monkeypatch, kernel):
+    if kernel == "vpage":
+        monkeypatch.setenv("PBGPU_KERNEL", "vpage")
     seq = Sequence.from_config(pc.get("c3_udp_var"))
     ctx.load_sequence(9, seq, pc.SEED_BASE)
     n = 3001
     fb = ctx.alloc_frames(*ctx.build_size(9, n))
     try:
-        assert ctx.kernel_name(9).startswith("pb_vline_kernel")
+        assert ctx.kernel_name(9).startswith("pb_%s_kernel" % kernel)
         for first in (5, 123457, 5):
             ctx.build(9, first, n, fb)
             fb.fill_offsets()
