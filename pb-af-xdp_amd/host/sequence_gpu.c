@@ -195,6 +195,13 @@ typedef struct shared_umem
     int fd;         /* thread 0's socket, once open (-1 before; -2 if it failed) */
     pthread_mutex_t mu;
     pthread_cond_t cv;
+    /* --queue with several threads: every socket on the owner's queue, reaping the owner's
+     * completion ring (pb_xsk_shared_cq_t); the owner's socket stays open until the last
+     * thread is done with the ring */
+    int one_queue;
+    pb_xsk_shared_cq_t scq;
+    pb_xsk_t owner;
+    int owner_open;
 } shared_umem_t;
 
 typedef struct worker_arg
@@ -216,6 +223,10 @@ static void shared_release(shared_umem_t *u)
     pthread_mutex_unlock(&u->mu);
     if (last)
     {
+        if (u->owner_open)
+            pb_xsk_close(&u->owner);
+        if (u->one_queue)
+            pb_xsk_scq_free(&u->scq);
         pthread_mutex_destroy(&u->mu);
         pthread_cond_destroy(&u->cv);
         free(u->base);
@@ -449,8 +460,10 @@ static void *gpu_worker(void *p)
                 goto out;
             }
         }
+        pb_xsk_shared_cq_t *scq = w->shared && w->shared->one_queue ? &w->shared->scq : NULL;
         rc = pb_xsk_open(&xsk, w->device, q, umem_base, nslots, PB_FRAME_SIZE, bf, shared_fd, slot_base,
-                         w->shared ? umem_frames : nslots, w->cmd.queue_set ? (uint32_t)w->cmd.queue : 0u);
+                         w->shared ? umem_frames : nslots, w->cmd.queue_set ? (uint32_t)w->cmd.queue : 0u, scq,
+                         (uint32_t)w->shard);
         if (w->shared && w->shard == 0)
         {
             pthread_mutex_lock(&w->shared->mu);
@@ -465,7 +478,9 @@ static void *gpu_worker(void *p)
             goto out;
         }
     }
-    else if ((rc = pb_xsk_loopback(&xsk, umem_base, nslots, PB_FRAME_SIZE)) != 0)
+    else if ((rc = w->shared && w->shared->one_queue
+                       ? pb_xsk_loopback_shared(&xsk, umem_base, PB_FRAME_SIZE, &w->shared->scq, (uint32_t)w->shard)
+                       : pb_xsk_loopback(&xsk, umem_base, nslots, PB_FRAME_SIZE)) != 0)
     {
         last_error = rc;
         goto out;
@@ -688,7 +703,16 @@ out:
         pthread_cond_broadcast(&w->shared->cv);
         pthread_mutex_unlock(&w->shared->mu);
     }
-    pb_xsk_close(&xsk);
+    if (w->shared && w->shared->one_queue && w->shard == 0 && xsk.fd >= 0)
+    {
+        /* the owner's completion ring serves the other sockets until they are done */
+        pthread_mutex_lock(&w->shared->mu);
+        w->shared->owner = xsk;
+        w->shared->owner_open = 1;
+        pthread_mutex_unlock(&w->shared->mu);
+    }
+    else
+        pb_xsk_close(&xsk);
     if (umem)
     {
         if (registered)
@@ -741,15 +765,6 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
             return;
         }
     }
-    if (cmd.shared_umem && cmd.queue_set && t_cnt > 1 && cmd.tx && strcmp(cmd.tx, "xsk") == 0)
-    {
-        /* every thread on one queue: their sockets would have to share the owner's fill /
-         * completion rings (pb_xsk_open); refuse instead of failing threads 1..n-1 at bind */
-        fprintf(stderr, "[%d] --sharedumem with --queue binds all %d threads to queue %d: use one thread, or "
-                        "drop --queue (thread t then takes queue t).\n", seq_cnt + 1, t_cnt, cmd.queue);
-        last_error = PBGPU_EINVAL;
-        return;
-    }
     const uint16_t idx = seq_cnt++;
     start_time[idx] = time(NULL);
     shared_umem_t *shared = NULL;
@@ -779,6 +794,21 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
         }
         memset(shared->base, 0, (size_t)umem_frames * PB_FRAME_SIZE);
         shared->slots = slots;
+        /* --queue with several threads: every socket binds the owner's queue (af_xdp.c:443) and
+         * they share its completion ring */
+        if (cmd.queue_set && t_cnt > 1)
+        {
+            const int loop = !(cmd.tx && strcmp(cmd.tx, "xsk") == 0);
+            const int src = pb_xsk_scq_init(&shared->scq, (uint32_t)t_cnt, slots, PB_FRAME_SIZE, loop);
+            if (src != 0)
+            {
+                free(shared->base);
+                free(shared);
+                last_error = src;
+                return;
+            }
+            shared->one_queue = 1;
+        }
         shared->fd = -1;
         shared->refs = 1; /* seq_send's own reference, dropped after the threads are started */
         pthread_mutex_init(&shared->mu, NULL);

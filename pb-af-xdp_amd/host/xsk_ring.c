@@ -147,15 +147,63 @@ int pb_xsk_loopback(pb_xsk_t *x, uint8_t *umem, uint32_t n_frames, uint32_t fram
     return 0;
 }
 
+int pb_xsk_scq_init(pb_xsk_shared_cq_t *q, uint32_t n_threads, uint32_t slots, uint32_t frame_size, int loopback)
+{
+    if (q == NULL || n_threads == 0 || n_threads > PB_XSK_MAX_SHARERS || slots == 0 || (slots & (slots - 1)) ||
+        frame_size == 0)
+        return -EINVAL;
+    memset(q, 0, sizeof *q);
+    q->slots = slots;
+    q->frame_size = frame_size;
+    q->n_threads = n_threads;
+    if (loopback)
+    {
+        uint32_t n = 1;
+        while (n < n_threads * slots)
+            n <<= 1;
+        q->mem = calloc(1, 192 + (size_t)n * sizeof(uint64_t));
+        if (q->mem == NULL)
+            return -ENOMEM;
+        loop_ring(&q->cq, (uint8_t *)q->mem, n, 0);
+    }
+    pthread_mutex_init(&q->mu, NULL);
+    return 0;
+}
+
+void pb_xsk_scq_free(pb_xsk_shared_cq_t *q)
+{
+    if (q == NULL)
+        return;
+    pthread_mutex_destroy(&q->mu);
+    free(q->mem);
+    q->mem = NULL;
+}
+
+int pb_xsk_loopback_shared(pb_xsk_t *x, uint8_t *umem, uint32_t frame_size, pb_xsk_shared_cq_t *scq,
+                           uint32_t thread)
+{
+    if (scq == NULL || scq->mem == NULL || thread >= scq->n_threads)
+        return -EINVAL;
+    const int rc = pb_xsk_loopback(x, umem, scq->slots, frame_size);
+    if (rc)
+        return rc;
+    x->scq = scq;
+    x->thread = thread;
+    x->slot_base = thread * scq->slots;
+    return 0;
+}
+
 uint32_t pb_xsk_loop_consume(pb_xsk_t *x, uint32_t max, pb_xsk_sink_fn sink, void *ctx)
 {
     /* the kernel's side of both rings: consumer of TX, producer of completions.
      * It keeps no cached indices of its own: it reads TX's producer and the
      * completion ring's consumer (both written by the application) each call. */
+    /* (a queue sharing a UMEM posts to the shared completion ring: the caller holds scq->mu) */
+    pb_xsk_ring_t *const cq = x->scq ? &x->scq->cq : &x->cq;
     const uint32_t tx_prod = load_acquire(x->tx.producer);
     const uint32_t tx_cons = *x->tx.consumer;
-    const uint32_t cq_prod = *x->cq.producer;
-    const uint32_t cq_free = x->cq.size - (cq_prod - load_acquire(x->cq.consumer));
+    const uint32_t cq_prod = *cq->producer;
+    const uint32_t cq_free = cq->size - (cq_prod - load_acquire(cq->consumer));
     uint32_t n = tx_prod - tx_cons;
     if (n > max)
         n = max;
@@ -166,12 +214,12 @@ uint32_t pb_xsk_loop_consume(pb_xsk_t *x, uint32_t max, pb_xsk_sink_fn sink, voi
         const struct xdp_desc *d = &((const struct xdp_desc *)x->tx.ring)[(tx_cons + i) & x->tx.mask];
         if (sink)
             sink(ctx, x->umem + d->addr, d->len, d->addr);
-        ((uint64_t *)x->cq.ring)[(cq_prod + i) & x->cq.mask] = d->addr;
+        ((uint64_t *)cq->ring)[(cq_prod + i) & cq->mask] = d->addr;
     }
     if (n)
     {
         store_release(x->tx.consumer, tx_cons + n); /* TX entries read: free for the producer */
-        store_release(x->cq.producer, cq_prod + n); /* completions written: visible to the reaper */
+        store_release(cq->producer, cq_prod + n);   /* completions written: visible to the reaper */
     }
     return n;
 }
@@ -200,20 +248,22 @@ static int map_ring(int fd, pb_xsk_ring_t *r, const struct xdp_ring_offset *off,
 
 int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, uint32_t n_frames,
                 uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames,
-                uint32_t shared_queue)
+                uint32_t shared_queue, pb_xsk_shared_cq_t *scq, uint32_t thread)
 {
     if (x == NULL || ifname == NULL || umem == NULL || n_frames == 0 || (n_frames & (n_frames - 1)) ||
         slot_base + n_frames > (umem_frames ? umem_frames : n_frames))
         return -EINVAL;
     /* xsk_bind: XDP_SHARED_UMEM on the owner's (device, queue) shares its buffer pool and
-     * rejects a socket with fill / completion rings of its own; these per-thread rings need
-     * another queue (libxdp's xsk_socket__create_shared handles the same-queue case by
-     * sharing the owner's rings between sockets, which this reaper does not) */
-    if (shared_fd >= 0 && shared_queue == queue)
+     * rejects a socket with fill / completion rings of its own: such a socket takes none and
+     * reaps the owner's completion ring through scq (xsk_socket__create_shared's model) */
+    const int on_owner_queue = shared_fd >= 0 && shared_queue == queue;
+    if (on_owner_queue && scq == NULL)
         return -EINVAL;
     memset(x, 0, sizeof *x);
     x->fd = -1;
     x->slot_base = slot_base;
+    x->scq = scq;
+    x->thread = thread;
     const unsigned ifindex = if_nametoindex(ifname);
     if (ifindex == 0)
         return -ENODEV;
@@ -233,9 +283,11 @@ int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, 
     mr.chunk_size = frame_size;
     int rc = 0;
     const int ring_n = (int)n_frames;
+    /* the owner's fill and completion rings cover the whole UMEM when queues share it */
+    const int cq_n = (int)(scq && shared_fd < 0 ? (umem_frames ? umem_frames : n_frames) : n_frames);
     if ((shared_fd < 0 && setsockopt(fd, SOL_XDP, XDP_UMEM_REG, &mr, sizeof mr)) ||
-        setsockopt(fd, SOL_XDP, XDP_UMEM_FILL_RING, &ring_n, sizeof ring_n) ||
-        setsockopt(fd, SOL_XDP, XDP_UMEM_COMPLETION_RING, &ring_n, sizeof ring_n) ||
+        (!on_owner_queue && (setsockopt(fd, SOL_XDP, XDP_UMEM_FILL_RING, &cq_n, sizeof cq_n) ||
+                             setsockopt(fd, SOL_XDP, XDP_UMEM_COMPLETION_RING, &cq_n, sizeof cq_n))) ||
         /* xsk_socket__create with a TX ring only (af_xdp.c:103-165) */
         setsockopt(fd, SOL_XDP, XDP_TX_RING, &ring_n, sizeof ring_n))
     {
@@ -250,11 +302,13 @@ int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, 
         goto fail;
     }
     if ((rc = map_ring(fd, &x->tx, &off.tx, n_frames, sizeof(struct xdp_desc), XDP_PGOFF_TX_RING, 1, &x->maps[0],
-                       &x->map_len[0])) ||
-        (rc = map_ring(fd, &x->cq, &off.cr, n_frames, sizeof(uint64_t), XDP_UMEM_PGOFF_COMPLETION_RING, 0, &x->maps[1],
-                       &x->map_len[1])) ||
-        (rc = map_ring(fd, &x->fq, &off.fr, n_frames, sizeof(uint64_t), XDP_UMEM_PGOFF_FILL_RING, 1, &x->maps[2],
-                       &x->map_len[2])))
+                       &x->map_len[0])))
+        goto fail;
+    if (!on_owner_queue &&
+        ((rc = map_ring(fd, &x->cq, &off.cr, (uint32_t)cq_n, sizeof(uint64_t), XDP_UMEM_PGOFF_COMPLETION_RING, 0,
+                        &x->maps[1], &x->map_len[1])) ||
+         (rc = map_ring(fd, &x->fq, &off.fr, (uint32_t)cq_n, sizeof(uint64_t), XDP_UMEM_PGOFF_FILL_RING, 1,
+                        &x->maps[2], &x->map_len[2]))))
         goto fail;
     struct sockaddr_xdp sxdp;
     memset(&sxdp, 0, sizeof sxdp);
@@ -273,6 +327,13 @@ int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, 
         goto fail;
     }
     x->need_wakeup = (bind_flags & XDP_USE_NEED_WAKEUP) != 0;
+    if (scq && shared_fd < 0)
+    {
+        /* the owner: its completion ring is the one every socket of the queue reaps */
+        pthread_mutex_lock(&scq->mu);
+        scq->cq = x->cq;
+        pthread_mutex_unlock(&scq->mu);
+    }
     return 0;
 fail:
     pb_xsk_close(x);
@@ -300,12 +361,13 @@ uint32_t pb_xsk_complete(pb_xsk_t *x, uint32_t max)
     if (!x->outstanding_tx)
         return 0;
     /* wake the kernel: always without need-wakeup, else only when it asks (af_xdp.c:38-41) */
-    if (!x->need_wakeup || pb_ring_needs_wakeup(&x->tx))
+    const int wake = !x->need_wakeup || pb_ring_needs_wakeup(&x->tx);
+    if (wake)
     {
         ++x->wakeups;
         if (x->fd >= 0)
             (void)sendto(x->fd, NULL, 0, MSG_DONTWAIT, NULL, 0);
-        else if (x->loop_auto)
+        else if (x->loop_auto && !x->scq) /* (a shared ring's kernel side runs under its lock, below) */
         {
             const uint32_t pending = __atomic_load_n(x->tx.producer, __ATOMIC_ACQUIRE) - *x->tx.consumer;
             if (pending > x->loop_hold)
@@ -313,6 +375,37 @@ uint32_t pb_xsk_complete(pb_xsk_t *x, uint32_t max)
         }
     }
     uint32_t idx = 0;
+    if (x->scq)
+    {
+        /* the shared completion ring: reap every entry, credit each to its slot range's thread,
+         * take this thread's credits (at most its outstanding frames, which bounds them) */
+        pb_xsk_shared_cq_t *q = x->scq;
+        pthread_mutex_lock(&q->mu);
+        if (x->fd < 0 && x->loop_auto && wake)
+        {
+            const uint32_t pending = __atomic_load_n(x->tx.producer, __ATOMIC_ACQUIRE) - *x->tx.consumer;
+            if (pending > x->loop_hold)
+                (void)pb_xsk_loop_consume(x, pending - x->loop_hold, x->loop_sink, x->loop_ctx);
+        }
+        uint32_t got;
+        while ((got = pb_ring_cons_peek(&q->cq, q->cq.size, &idx)) != 0)
+        {
+            for (uint32_t i = 0; i < got; ++i)
+            {
+                const uint64_t t = pb_ring_comp_addr(&q->cq, idx + i) / q->frame_size / q->slots;
+                if (t < q->n_threads)
+                    ++q->credit[t];
+            }
+            pb_ring_cons_release(&q->cq, got);
+            q->reaped += got;
+        }
+        const uint32_t n = q->credit[x->thread];
+        q->credit[x->thread] = 0;
+        pthread_mutex_unlock(&q->mu);
+        x->outstanding_tx -= n;
+        x->completed += n;
+        return n;
+    }
     const uint32_t n = pb_ring_cons_peek(&x->cq, max, &idx);
     if (n)
     {

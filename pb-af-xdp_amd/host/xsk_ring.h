@@ -23,6 +23,7 @@
  */
 #pragma once
 
+#include <pthread.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -57,6 +58,31 @@ uint32_t pb_ring_cons_peek(pb_xsk_ring_t *r, uint32_t nb, uint32_t *idx);
 uint64_t pb_ring_comp_addr(const pb_xsk_ring_t *r, uint32_t idx);
 void pb_ring_cons_release(pb_xsk_ring_t *r, uint32_t nb);
 
+/* ---- --sharedumem with every socket on one queue (af_xdp.c:412-443) ----
+ * The kernel binds a second socket of a UMEM to the owner's (device, queue) only on the owner's
+ * fill and completion rings (libbpf's xsk_socket__create_shared on the same queue): every
+ * socket's TX completions arrive on the owner's one completion ring.  Whichever thread reaps it
+ * does so under `mu` and credits each completion to the thread whose slot range holds its
+ * address; a thread takes its credits when it reaps. */
+#define PB_XSK_MAX_SHARERS 256
+typedef struct pb_xsk_shared_cq
+{
+    pthread_mutex_t mu;
+    pb_xsk_ring_t cq;      /* the owner's completion ring (socket: its mapping; loopback: `mem`) */
+    uint32_t slots;        /* UMEM slots per thread (thread t: [t * slots, (t + 1) * slots)) */
+    uint32_t frame_size;
+    uint32_t n_threads;
+    uint32_t credit[PB_XSK_MAX_SHARERS]; /* per thread: completions reaped for it, not yet taken */
+    void *mem;             /* loopback: the ring's backing memory */
+    uint64_t reaped;       /* completions taken off the ring, all threads */
+} pb_xsk_shared_cq_t;
+
+/* Set up q for n_threads threads of `slots` slots of frame_size bytes; loopback != 0: the ring
+ * lives in ordinary memory (a power of two >= n_threads * slots entries), else pb_xsk_open of
+ * the owner (thread 0) maps it.  Returns 0 or -errno. */
+int pb_xsk_scq_init(pb_xsk_shared_cq_t *q, uint32_t n_threads, uint32_t slots, uint32_t frame_size, int loopback);
+void pb_xsk_scq_free(pb_xsk_shared_cq_t *q);
+
 /* ---- one TX queue: UMEM + TX ring + completion ring ---- */
 typedef struct pb_xsk
 {
@@ -82,6 +108,8 @@ typedef struct pb_xsk
     uint32_t loop_hold;      /* loopback (tests): the kernel side leaves the newest loop_hold descriptors
                                 unconsumed, as a slow NIC would keep frames in flight */
     uint32_t slot_base;      /* first UMEM slot of this queue's ring (--sharedumem: queues share one UMEM) */
+    pb_xsk_shared_cq_t *scq; /* --sharedumem on one queue: the completion ring every socket shares */
+    uint32_t thread;         /* this queue's thread index in scq */
 } pb_xsk_t;
 
 /* Loopback TX queue of n_frames (a power of two) slots of frame_size bytes over
@@ -90,6 +118,11 @@ typedef struct pb_xsk
  * descriptors, as a wakeup would (set loop_sink to see the frames); tests that
  * run the kernel side on a thread of their own clear it. */
 int pb_xsk_loopback(pb_xsk_t *x, uint8_t *umem, uint32_t n_frames, uint32_t frame_size);
+/* The same, one of several queues on one UMEM sharing scq's completion ring (its kernel side
+ * posts there; scq->mu held): thread t's ring covers UMEM slots [t * scq->slots, ...), n_frames
+ * = scq->slots. */
+int pb_xsk_loopback_shared(pb_xsk_t *x, uint8_t *umem, uint32_t frame_size, pb_xsk_shared_cq_t *scq,
+                           uint32_t thread);
 /* The loopback's kernel side: take up to max TX descriptors, hand each to
  * `sink` (may be NULL), post their addresses to the completion ring.  Returns
  * the number moved. */
@@ -104,12 +137,14 @@ uint32_t pb_xsk_loop_consume(pb_xsk_t *x, uint32_t max, pb_xsk_sink_fn sink, voi
  * slots from slot_base on.  shared_queue: the queue the owner socket is bound
  * to.  The kernel lets a shared-UMEM socket keep rings of its own only on
  * another queue (or device); on the owner's queue it must use the owner's
- * fill / completion rings, which a per-thread reaper cannot share, so that
- * case is refused with -EINVAL before any socket is made.  Returns 0, or
- * -errno (EPERM without CAP_NET_RAW, EAFNOSUPPORT without AF_XDP). */
+ * fill / completion rings: that needs scq (pb_xsk_shared_cq_t), which the
+ * owner (shared_fd < 0, scq set) publishes its completion ring into and the
+ * others reap through; without scq that case is refused with -EINVAL before
+ * any socket is made.  Returns 0, or -errno (EPERM without CAP_NET_RAW,
+ * EAFNOSUPPORT without AF_XDP). */
 int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, uint32_t n_frames,
                 uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames,
-                uint32_t shared_queue);
+                uint32_t shared_queue, pb_xsk_shared_cq_t *scq, uint32_t thread);
 void pb_xsk_close(pb_xsk_t *x);
 
 /* complete_tx() (af_xdp.c:25-53): wake the kernel if it asks (or always without

@@ -70,7 +70,7 @@ class Xsk(C.Structure):
                 ("need_wakeup", C.c_uint32), ("wakeups", C.c_uint64), ("completed", C.c_uint64),
                 ("maps", C.c_void_p * 3), ("map_len", C.c_size_t * 3), ("loop_mem", C.c_void_p),
                 ("loop_auto", C.c_int), ("loop_sink", C.c_void_p), ("loop_ctx", C.c_void_p), ("batch", C.c_uint32),
-                ("loop_hold", C.c_uint32), ("slot_base", C.c_uint32)]
+                ("loop_hold", C.c_uint32), ("slot_base", C.c_uint32), ("scq", C.c_void_p), ("thread", C.c_uint32)]
 
 
 def _loopback(host, n, fs=4096):
@@ -144,31 +144,55 @@ def test_af_xdp_socket_setup_fails_cleanly_without_privilege(libs):
     x = Xsk()
     umem = np.zeros(4096 * 4096 + 4096, dtype=np.uint8)
     base = (umem.ctypes.data + 4095) & ~4095
-    rc = host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096, 0)
+    rc = host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096, 0, None, 0)
     # a negative errno (no AF_XDP / CAP_NET_RAW in this container), or a bound socket
     assert rc <= 0
     if rc == 0:
         host.pb_xsk_close(C.byref(x))
-    assert host.pb_xsk_open(C.byref(x), b"pbnodev0", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096, 0) == -19  # -ENODEV
+    assert host.pb_xsk_open(C.byref(x), b"pbnodev0", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096, 0, None, 0) == -19  # -ENODEV
     # a shared-UMEM socket's slot range must lie inside the UMEM
-    assert host.pb_xsk_open(C.byref(x), b"lo", 1, C.c_void_p(base), 2048, 4096, 0, 3, 4096, 4096, 0) == -22
+    assert host.pb_xsk_open(C.byref(x), b"lo", 1, C.c_void_p(base), 2048, 4096, 0, 3, 4096, 4096, 0, None, 0) == -22
 
 
-def test_shared_umem_socket_on_the_owners_queue_is_refused(libs):
+def test_shared_umem_socket_on_the_owners_queue_needs_the_shared_ring(libs):
     """xsk_bind lets an XDP_SHARED_UMEM socket keep its own fill / completion rings only
-    on another queue or device; on the owner's queue it must take the owner's rings
-    (a shared buffer pool), which per-thread reapers cannot share.  pb_xsk_open refuses
-    that combination up front, and seq_send refuses --sharedumem --queue with several
-    threads instead of letting threads 1..n-1 fail at bind."""
+    on another queue or device; on the owner's queue it must take the owner's rings (a
+    shared buffer pool).  pb_xsk_open refuses that combination without a shared completion
+    ring (pb_xsk_shared_cq_t) before any socket is made; seq_send now gives --sharedumem
+    --queue with several threads that ring, so the sequence gets as far as the socket (which
+    this container cannot open: no AF_XDP / CAP_NET_RAW)."""
     host, _ = libs
     x = Xsk()
     umem = np.zeros(4096 * 4096 + 4096, dtype=np.uint8)
     base = (umem.ctypes.data + 4095) & ~4095
-    # a valid slot range (2048 slots from 2048 of 4096), shared fd, the owner's queue 5
-    assert host.pb_xsk_open(C.byref(x), b"lo", 5, C.c_void_p(base), 2048, 4096, 0, 3, 2048, 4096, 5) == -22
+    # a valid slot range (2048 slots from 2048 of 4096), shared fd, the owner's queue 5, no ring
+    assert host.pb_xsk_open(C.byref(x), b"lo", 5, C.c_void_p(base), 2048, 4096, 0, 3, 2048, 4096, 5, None, 1) == -22
     assert x.fd == 0 and x.umem is None  # refused before any socket was made
     r = _run(libs, _cfg(maxpckts=1000, delay=0, threads=2), shared_umem=1, queue=5, queue_set=1, tx=b"xsk")
-    assert r["err"] == -22 and r["seen"] == 0 and r["pckts"] == 0
+    assert r["err"] != 0 and r["pckts"] == 0  # the socket open fails here, not a refusal up front
+
+
+@pytest.mark.parametrize("threads,hold", [(3, 0), (4, 7), (2, 0)])
+def test_sharedumem_one_queue_shares_the_completion_ring(libs, monkeypatch, threads, hold):
+    """--sharedumem --queue 0 with several threads (af_xdp.c:412-443: every socket on the
+    owner's queue): all threads' completions arrive on one ring, reaped under a lock and
+    credited to the thread whose slot range holds each address.  On the loopback every frame
+    is submitted once, the quota is exact and every descriptor completes; PB_LOOP_HOLD keeps
+    some frames in flight so reaps interleave across threads."""
+    host = libs[0]
+    if hold:
+        monkeypatch.setenv("PB_LOOP_HOLD", str(hold))
+    r = _run(libs, _cfg(maxpckts=30000, delay=0, threads=threads), gpu_batch=1000, shared_umem=1, queue=0,
+             queue_set=1)
+    assert r["err"] == 0 and r["pckts"] == 30000 and r["seen"] == 30000
+    assert len(np.unique(r["k"])) == 30000 and set(np.unique(r["thread"])) == set(range(threads))
+    assert (r["len"] != 0xFFFF).all()  # every descriptor's frame intact in its slot
+    d, c, wk = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    host.pb_sequence_tx_stats(0, C.byref(d), C.byref(c), C.byref(wk))
+    assert d.value == 30000 and c.value == 30000
+    u = C.c_uint64()
+    host.pb_sequence_umems(0, C.byref(u))
+    assert u.value == 1
 
 
 def test_gpu_range_past_the_device_count_is_refused_up_front(libs):
