@@ -2345,8 +2345,14 @@ static int land_unmapped(pbgpu_ctx *ctx, const pbgpu_frames *f, uint8_t *dst, ui
     hipStream_t ls = ctx->land_stream;
     if (f->fixed_len)
     {
-        HIPCHK(hipMemcpy2DAsync(dst, slot_stride, f->data + first_frame * f->fixed_len, f->fixed_len, f->fixed_len,
-                                n, hipMemcpyDeviceToHost, ls));
+        // strided DMA in runs of at most 32768 rows (a 2^18-row copy failed on the runtime)
+        for (uint32_t i = 0; i < n; i += 32768)
+        {
+            const uint32_t rows = n - i < 32768 ? n - i : 32768;
+            HIPCHK(hipMemcpy2DAsync(dst + (uint64_t)i * slot_stride, slot_stride,
+                                    f->data + (first_frame + i) * f->fixed_len, f->fixed_len, f->fixed_len, rows,
+                                    hipMemcpyDeviceToHost, ls));
+        }
         HIPCHK(hipStreamSynchronize(ls));
         if (lens_out)
             for (uint32_t i = 0; i < n; ++i)

@@ -9,52 +9,77 @@ import json
 import os
 import sys
 
-out_dir = sys.argv[1]
-res = {"per_launch_hbm_bytes": {}, "per_launch": {}, "note": __doc__}
-for d in sorted(glob.glob(os.path.join(out_dir, "pmc_*"))):
-    if not os.path.isdir(d):
-        continue
-    name = os.path.basename(d)[4:]
-    cfg = name
-    for tag in ("_write_size", "_fetch_size", "_sq_waves", "_sq_lds_bank_conflict"):
-        if name.endswith(tag):
-            cfg = name[: -len(tag)]
-    for f in glob.glob(os.path.join(d, "run_counter_collection.csv")):
-        agg = collections.defaultdict(list)
-        rows = list(csv.DictReader(open(f)))
-        isbuild = lambda kn: kn.startswith("void pb_") and any(  # noqa: E731
-            x in kn for x in ("gpf", "stage", "small", "xpage", "ximg", "vline", "batch", "fpage"))
-        # the build launches are the largest build-kernel grid; smaller ones are setup dispatches
-        # (pb_ximg_body's image pages, built once by pb_xpage_kernel at load)
-        gmax = max([int(r["Grid_Size"]) for r in rows if isbuild(r["Kernel_Name"])] or [0])
-        for r in rows:
-            kn = r["Kernel_Name"]
-            build = isbuild(kn)
-            if build and int(r["Grid_Size"]) < gmax:
-                continue
-            aux = kn.startswith("void pb_len_") or kn.startswith("pb_len_") or "pb_scan_blocks" in kn
-            fold = "pb_ctr_fold" in kn  # the counters' fold: its bytes spread over the build launches
-            aux = aux or fold
-            if not (build or aux):
-                continue
-            agg[(kn, r["Counter_Name"], aux)].append(float(r["Counter_Value"]))
-        builds = {cn: len(v) for (kn, cn, aux), v in agg.items() if not aux}
-        for (kn, cn, aux), v in agg.items():
-            e = res["per_launch"].setdefault(cfg, {"kernel": None, "aux": {}})
-            if aux and "pb_ctr_fold" in kn:  # amortized: its total over the run's build launches
-                e["aux"].setdefault(kn, {})[cn] = sum(v) / max(1, builds.get(cn, len(v)))
-            elif aux:  # the length scan of variable-length frames: part of each step's traffic
-                e["aux"].setdefault(kn, {})[cn] = sum(v) / len(v)
-            else:
-                e["kernel"] = kn
-                e[cn] = sum(v) / len(v)
-for cfg, e in res["per_launch"].items():
-    if "WRITE_SIZE" in e:
-        hb = e["WRITE_SIZE"] * 1024 + 2 * e.get("FETCH_SIZE", 0) * 1024
-        for a in e["aux"].values():
-            hb += a.get("WRITE_SIZE", 0) * 1024 + 2 * a.get("FETCH_SIZE", 0) * 1024
-        res["per_launch_hbm_bytes"][cfg] = int(hb)
-        # (c5_mix: 2^24 iterations of each of its three sequences per fused launch)
-        res.setdefault("packets_per_launch", {})[cfg] = 16777216 if cfg == "c5_mix" else 33554432
-json.dump(res, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
-print(json.dumps(res["per_launch_hbm_bytes"], indent=1))
+def setup_dispatches(rows, isbuild):
+    """Dispatch ids of build kernels that precede the kernel's first dispatch at its final grid."""
+    by_kernel = collections.defaultdict(dict)
+    for r in rows:
+        if isbuild(r["Kernel_Name"]):
+            by_kernel[r["Kernel_Name"]][int(r["Dispatch_Id"])] = int(r["Grid_Size"])
+    out = set()
+    for d in by_kernel.values():
+        ids = sorted(d)
+        final = d[ids[-1]]
+        for i in ids:
+            if d[i] == final:
+                break
+            out.add(str(i))
+    return out
+
+
+def main():
+    out_dir = sys.argv[1]
+    res = {"per_launch_hbm_bytes": {}, "per_launch": {}, "note": __doc__}
+    for d in sorted(glob.glob(os.path.join(out_dir, "pmc_*"))):
+        if not os.path.isdir(d):
+            continue
+        name = os.path.basename(d)[4:]
+        cfg = name
+        for tag in ("_write_size", "_fetch_size", "_sq_waves", "_sq_lds_bank_conflict"):
+            if name.endswith(tag):
+                cfg = name[: -len(tag)]
+        for f in glob.glob(os.path.join(d, "run_counter_collection.csv")):
+            agg = collections.defaultdict(list)
+            rows = list(csv.DictReader(open(f)))
+            isbuild = lambda kn: kn.startswith("void pb_") and any(  # noqa: E731
+                x in kn for x in ("gpf", "stage", "small", "xpage", "ximg", "vline", "vpage", "batch", "fpage"))
+            # load-time setup dispatches (pb_ximg_body's image pages, built once by pb_xpage_kernel in
+            # pbgpu_load_sequence) come before a kernel's first build launch: drop a build kernel's
+            # leading dispatches whose grid is not its last dispatch's (the bench's build size); every
+            # dispatch from its first build-size one on counts, whatever its grid
+            setup = setup_dispatches(rows, isbuild)
+            for r in rows:
+                kn = r["Kernel_Name"]
+                build = isbuild(kn)
+                if build and r["Dispatch_Id"] in setup:
+                    continue
+                aux = (kn.startswith("void pb_len_") or kn.startswith("pb_len_") or "pb_scan_blocks" in kn or
+                       "pb_vrec_kernel" in kn)  # (pb_vpage_kernel's record pass)
+                fold = "pb_ctr_fold" in kn  # the counters' fold: its bytes spread over the build launches
+                aux = aux or fold
+                if not (build or aux):
+                    continue
+                agg[(kn, r["Counter_Name"], aux)].append(float(r["Counter_Value"]))
+            builds = {cn: len(v) for (kn, cn, aux), v in agg.items() if not aux}
+            for (kn, cn, aux), v in agg.items():
+                e = res["per_launch"].setdefault(cfg, {"kernel": None, "aux": {}})
+                if aux and "pb_ctr_fold" in kn:  # amortized: its total over the run's build launches
+                    e["aux"].setdefault(kn, {})[cn] = sum(v) / max(1, builds.get(cn, len(v)))
+                elif aux:  # the length scan of variable-length frames: part of each step's traffic
+                    e["aux"].setdefault(kn, {})[cn] = sum(v) / len(v)
+                else:
+                    e["kernel"] = kn
+                    e[cn] = sum(v) / len(v)
+    for cfg, e in res["per_launch"].items():
+        if "WRITE_SIZE" in e:
+            hb = e["WRITE_SIZE"] * 1024 + 2 * e.get("FETCH_SIZE", 0) * 1024
+            for a in e["aux"].values():
+                hb += a.get("WRITE_SIZE", 0) * 1024 + 2 * a.get("FETCH_SIZE", 0) * 1024
+            res["per_launch_hbm_bytes"][cfg] = int(hb)
+            # (c5_mix: 2^24 iterations of each of its three sequences per fused launch)
+            res.setdefault("packets_per_launch", {})[cfg] = 16777216 if cfg == "c5_mix" else 33554432
+    json.dump(res, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
+    print(json.dumps(res["per_launch_hbm_bytes"], indent=1))
+
+
+if __name__ == "__main__":
+    main()

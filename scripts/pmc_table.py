@@ -9,6 +9,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_collect import setup_dispatches  # noqa: E402
+
 out = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(sys.argv[1], "pmc_*", "**", "*counter_collection.csv"), recursive=True):
     cfg = os.path.relpath(f, sys.argv[1]).split(os.sep)[0][4:]
@@ -16,12 +19,13 @@ for f in glob.glob(os.path.join(sys.argv[1], "pmc_*", "**", "*counter_collection
         cfg = cfg[: -len(g)] if cfg.endswith(g) else cfg
     rows = list(csv.DictReader(open(f)))
     want = lambda kn: kn.startswith("void pb_") and "len_" not in kn and "scan" not in kn and "fill" not in kn  # noqa
-    # the build launches: the largest grid (smaller ones are setup dispatches, e.g. pb_ximg_body's
-    # image pages built at load)
-    gmax = max([int(r["Grid_Size"]) for r in rows if want(r["Kernel_Name"])] or [0])
+    # load-time setup dispatches (pb_ximg_body's image pages built in pbgpu_load_sequence) precede a
+    # kernel's first build launch: a kernel's leading dispatches at another grid than its last
+    # dispatch's are dropped (pmc_collect.setup_dispatches), every later one counts
+    setup = setup_dispatches(rows, want)
     for r in rows:
         kn = r["Kernel_Name"]
-        if want(kn) and int(r["Grid_Size"]) == gmax:
+        if want(kn) and r["Dispatch_Id"] not in setup:
             out[(cfg, kn.split("(")[0][5:])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 res = {}
 for (cfg, kn), cs in sorted(out.items()):

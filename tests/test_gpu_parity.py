@@ -362,3 +362,25 @@ def test_jumbo_frames_refused_by_4k_slots(ctx):
             assert rc == -22
             assert (umem == 0xEE).all()
         fb.free()
+
+
+def test_unregistered_landing_of_a_large_batch(ctx):
+    """Fixed-length frames into unregistered memory land by strided DMA: a 2^18-frame batch (the
+    bench's D2H size) in runs of at most 32768 rows (one 2^18-row hipMemcpy2DAsync failed),
+    every frame in its 4 KiB slot and the slot bytes past it untouched."""
+    seq = Sequence.from_config(pc.get("c2_udp_64"))
+    ctx.load_sequence(9, seq, pc.SEED_BASE)
+    n = 1 << 18
+    fb = ctx.alloc_frames(*ctx.build_size(9, n))
+    ctx.build(9, 77, n, fb)
+    ctx.sync()
+    umem = np.full(4096 * n, 0xEE, dtype=np.uint8)
+    lens = fb.to_umem(umem, 4096, 0, n)
+    data = fb.packed()
+    fb.free()
+    assert (lens == 64).all()
+    slots = umem.reshape(n, 4096)
+    assert np.array_equal(slots[:, :64], data.reshape(n, 64))
+    assert (slots[::511, 64:] == 0xEE).all()
+    want = ob.frames(seq, 9, 77 + n - 40, 40, pc.SEED_BASE)
+    assert [slots[n - 40 + j, :64].tobytes() for j in range(40)] == want
