@@ -3,7 +3,7 @@
 # into profiles/$ROUND/$DEST (default prof/) and profiles/pmc_$ROUND.json.
 set -e
 cd "$(dirname "$0")/.."
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 SRC=gpurun_out/prof_$ROUND
 DST=profiles/$ROUND/${DEST:-prof}
 rm -rf $DST; mkdir -p $DST/cfg

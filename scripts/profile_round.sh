@@ -8,12 +8,12 @@
 # Output: gpurun_out/prof_$ROUND/ (copied to profiles/$ROUND/prof/ afterwards).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 OUT=gpurun_out/prof_$ROUND
 PMC=profiles/pmc_$ROUND.json
 [ -z "$KEEP_OUT" ] && rm -rf $OUT; mkdir -p $OUT/cfg
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > $OUT/pytest.log 2>&1
   rc=$?
   echo "rc=$rc" >> $OUT/pytest.log
   [ $rc -ne 0 ] && { tail -5 $OUT/pytest.log; exit $rc; }

@@ -384,3 +384,38 @@ def test_unregistered_landing_of_a_large_batch(ctx):
     assert (slots[::511, 64:] == 0xEE).all()
     want = ob.frames(seq, 9, 77 + n - 40, 40, pc.SEED_BASE)
     assert [slots[n - 40 + j, :64].tobytes() for j in range(40)] == want
+
+
+@pytest.mark.parametrize("dma_min", ["64", "100000"])
+@pytest.mark.parametrize("name", ["c2_udp_64", "c2_udp_1500", "c5_icmp_echo"])
+def test_umem_landing_dma_or_scatter(monkeypatch, name, dma_min):
+    """Registered UMEM, both landing paths whatever the length (PBGPU_LAND_DMA_MIN: fixed frames
+    of at least that many bytes go by strided DMA, the rest by the scatter kernel; 1024 by
+    default): every frame in its 4 KiB slot, the bytes past it untouched, over two queued
+    landings of 40,000 frames each (two 32768-row DMA runs)."""
+    monkeypatch.setenv("PBGPU_LAND_DMA_MIN", dma_min)
+    c = GpuContext(0)
+    try:
+        seq = Sequence.from_config(pc.get(name))
+        c.load_sequence(3, seq, pc.SEED_BASE)
+        n = 80000
+        fb = c.alloc_frames(*c.build_size(3, n))
+        c.build(3, 9, n, fb)
+        c.sync()
+        data = fb.packed()
+        flen = len(data) // n
+        umem = np.full(4096 * n, 0xEE, dtype=np.uint8)
+        assert c.lib.pbgpu_host_register(c.h, umem.ctypes.data, umem.nbytes) == 0
+        try:
+            lens_a = fb.to_umem(umem, 4096, 0, 40000)
+            lens_b = fb.to_umem(umem, 4096, 40000, 40000, first_slot=40000)
+        finally:
+            c.lib.pbgpu_host_unregister(c.h, umem.ctypes.data)
+        fb.free()
+        assert (lens_a == flen).all() and (lens_b == flen).all()
+        slots = umem.reshape(n, 4096)
+        assert np.array_equal(slots[:, :flen], data.reshape(n, flen))
+        assert (slots[::97, flen:] == 0xEE).all()
+        assert slots[n - 1, :flen].tobytes() == ob.frames(seq, 3, 9 + n - 1, 1, pc.SEED_BASE)[0]
+    finally:
+        c.close()
