@@ -41,7 +41,7 @@ from pbgpu import GpuContext, Sequence  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 HBM_ACHIEVABLE_GBPS = 6300.0  # the same guide's "≈6.3 TB/s achievable" (HBM section)
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r05.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r06.json")
 MIX = ("c2_udp_64", "c4_tcp_syn", "c5_icmp_echo")  # configs[4]'s three sequences (pb_configs.c5_mix)
 
 

@@ -10,20 +10,22 @@ import os
 import sys
 
 def setup_dispatches(rows, isbuild):
-    """Dispatch ids of build kernels that precede the kernel's first dispatch at its final grid."""
-    by_kernel = collections.defaultdict(dict)
+    """Dispatch ids of load-time setup launches: every build-kernel dispatch that comes before the
+    run's first build launch, i.e. the first dispatch of the most-dispatched build kernel at the
+    grid of its last dispatch (pbgpu_load_sequence's image pages run pb_xpage_kernel once, at
+    another grid, before the builds; in configs[4] before the fused pb_batch_kernel)."""
+    disp = {}
     for r in rows:
         if isbuild(r["Kernel_Name"]):
-            by_kernel[r["Kernel_Name"]][int(r["Dispatch_Id"])] = int(r["Grid_Size"])
-    out = set()
-    for d in by_kernel.values():
-        ids = sorted(d)
-        final = d[ids[-1]]
-        for i in ids:
-            if d[i] == final:
-                break
-            out.add(str(i))
-    return out
+            disp[int(r["Dispatch_Id"])] = (r["Kernel_Name"], int(r["Grid_Size"]))
+    if not disp:
+        return set()
+    count = collections.Counter(k for k, _ in disp.values())
+    main_k = count.most_common(1)[0][0]
+    ids = sorted(i for i, (k, _) in disp.items() if k == main_k)
+    final = disp[ids[-1]][1]
+    first = min(i for i in ids if disp[i][1] == final)
+    return {str(i) for i in disp if i < first}
 
 
 def main():
