@@ -116,8 +116,10 @@ struct pb_opts
     bool umem_dma = false;   // PBGPU_UMEM_DMA=1: land through DMA copies, not the mapped scatter
     bool alloc_vmm = true;   // PBGPU_ALLOC=malloc: frame buffers from hipMalloc (fb_alloc)
     uint32_t alloc_chunk_mb = 64; // PBGPU_ALLOC_CHUNK_MB: fb_alloc's physical chunk
-    uint32_t land_dma_min = 1024; // PBGPU_LAND_DMA_MIN: fixed frames of at least this many bytes land
-                                  // in registered UMEM by strided DMA instead of the scatter kernel
+    uint32_t land_dma_min = 0xFFFFFFFFu; // PBGPU_LAND_DMA_MIN: fixed frames of at least this many bytes
+                                  // land in registered UMEM by strided DMA instead of the scatter kernel
+                                  // (off by default: 1500 B read 56 vs 52 GB/s landing alone on one box,
+                                  // 43 vs 49 GB/s in bench.py's build + land on another)
     uint32_t vp_wgt = 0;       // PBGPU_VP_WGT=512: pb_vpage_kernel with 8 pages per workgroup
     uint32_t vp_pages_pct = 0; // PBGPU_VP_PAGES_PCT: pb_vpage_kernel's grid as a percentage of the
                                // expected pages (tests: a short grid, so waves take several pages)
@@ -2433,9 +2435,10 @@ int pbgpu_copy_to_umem_async(pbgpu_ctx *ctx, const pbgpu_frames *f, void *umem, 
     pbgpu_ctx::land_op op = {nullptr, lens_out, n, 0, f->fixed_len};
     if (f->fixed_len && f->fixed_len >= ctx->opt.land_dma_min)
     {
-        // long fixed frames: the copy engine, a strided DMA on the landing stream (1500 B, 2^18
-        // frames: 56.1 vs 52.2 GB/s for the scatter kernel; at 64 B the engine moves 218 Mpps
-        // against the kernel's 540, profiles/r06/d2h/), in runs of <= 32768 rows
+        // PBGPU_LAND_DMA_MIN: the copy engine, a strided DMA on the landing stream, in runs of
+        // <= 32768 rows (1500 B, 2^18 frames: 56.1 vs 52.2 GB/s for the scatter kernel landing
+        // alone, 43.1 vs 49.2 in bench.py's build + land; at 64 B the engine moves 218 Mpps against
+        // the kernel's 540, profiles/r06/d2h/)
         for (uint32_t i = 0; i < n; i += 32768)
         {
             const uint32_t rows = n - i < 32768 ? n - i : 32768;

@@ -89,17 +89,18 @@ __global__ __launch_bounds__(256) void pr6_rec_kernel(pb_kargs K, uint2 *rec, ui
     }
 }
 
-template <int XMAP, int LOADS>
-__global__ __launch_bounds__(256) void pr6_gate(uint8_t *out, const uint2 *pt, const uint2 *rec, uint64_t n,
+template <int XMAP, int LOADS, int WGT = 256>
+__global__ __launch_bounds__(WGT) void pr6_gate(uint8_t *out, const uint2 *pt, const uint2 *rec, uint64_t n,
                                                 uint32_t npages)
 {
+    constexpr uint32_t NW = WGT / 64;
     const uint32_t b = blockIdx.x, lane = threadIdx.x & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t c;
     if (XMAP == 0)
-        c = ((b >> 3) * 4u + wv) * 8u + (b & 7u);
+        c = ((b >> 3) * NW + wv) * 8u + (b & 7u);
     else
-        c = pb_xcd_region(b, gridDim.x) * 4u + wv;
+        c = pb_xcd_region(b, gridDim.x) * NW + wv;
     if (c >= npages)
         return;
     pb_u32x4 v;
@@ -304,6 +305,17 @@ int pr6_gate_run(pbgpu_ctx *ctx, void *dst, uint64_t total, uint64_t n, int vari
         case 1: hipLaunchKernelGGL((pr6_gate<1, 1>), g1, dim3(256), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
         case 2: hipLaunchKernelGGL((pr6_gate<0, 0>), g0, dim3(256), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
         case 3: hipLaunchKernelGGL((pr6_gate<1, 0>), g1, dim3(256), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
+        // store shapes without loads: pages per workgroup 1, 2, 8 (64-, 128-, 512-thread workgroups)
+        case 4: hipLaunchKernelGGL((pr6_gate<0, 0, 64>), dim3((np + 7) / 8 * 8), dim3(64), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
+        case 5: hipLaunchKernelGGL((pr6_gate<1, 0, 64>), dim3(np), dim3(64), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
+        case 6: hipLaunchKernelGGL((pr6_gate<0, 0, 128>), dim3((np + 15) / 16 * 8), dim3(128), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
+        case 7: hipLaunchKernelGGL((pr6_gate<1, 0, 128>), dim3((np + 1) / 2), dim3(128), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
+        case 8: hipLaunchKernelGGL((pr6_gate<0, 0, 512>), dim3((np + 63) / 64 * 8), dim3(512), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
+        case 9: hipLaunchKernelGGL((pr6_gate<1, 0, 512>), dim3((np + 7) / 8), dim3(512), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
+        // the same shapes with the loads
+        case 10: hipLaunchKernelGGL((pr6_gate<0, 1, 64>), dim3((np + 7) / 8 * 8), dim3(64), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
+        case 11: hipLaunchKernelGGL((pr6_gate<0, 1, 128>), dim3((np + 15) / 16 * 8), dim3(128), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
+        case 12: hipLaunchKernelGGL((pr6_gate<0, 1, 512>), dim3((np + 63) / 64 * 8), dim3(512), lds_pad, st, o, B6.pt, B6.rec, n, np); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

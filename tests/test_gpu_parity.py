@@ -390,9 +390,9 @@ def test_unregistered_landing_of_a_large_batch(ctx):
 @pytest.mark.parametrize("name", ["c2_udp_64", "c2_udp_1500", "c5_icmp_echo"])
 def test_umem_landing_dma_or_scatter(monkeypatch, name, dma_min):
     """Registered UMEM, both landing paths whatever the length (PBGPU_LAND_DMA_MIN: fixed frames
-    of at least that many bytes go by strided DMA, the rest by the scatter kernel; 1024 by
-    default): every frame in its 4 KiB slot, the bytes past it untouched, over two queued
-    landings of 40,000 frames each (two 32768-row DMA runs)."""
+    of at least that many bytes go by strided DMA, the rest by the scatter kernel, the default):
+    every frame in its 4 KiB slot, the bytes past it untouched, over two queued landings of
+    40,000 frames each (two 32768-row DMA runs)."""
     monkeypatch.setenv("PBGPU_LAND_DMA_MIN", dma_min)
     c = GpuContext(0)
     try:
