@@ -22,9 +22,12 @@ ctx = GpuContext(0)
 seq = Sequence.from_config(pc.get("c3_udp_var"))
 names = {}
 for i, v in enumerate(VARS):
-    # a variant is a PBGPU_KERNEL value, optionally with PBGPU_VP_WGT after a colon (vpage:512)
+    # a variant is a PBGPU_KERNEL value, optionally with PBGPU_VP_WGT after a colon (vpage:512), or
+    # vpage:pool for PBGPU_VP_POOL=1
     kern, _, wgt = v.partition(":")
-    for key, val in (("PBGPU_KERNEL", kern), ("PBGPU_VP_WGT", wgt)):
+    pool = "1" if wgt == "pool" else ""
+    wgt = "" if pool else wgt
+    for key, val in (("PBGPU_KERNEL", kern), ("PBGPU_VP_WGT", wgt), ("PBGPU_VP_POOL", pool)):
         if val:
             os.environ[key] = val
         else:
@@ -33,6 +36,7 @@ for i, v in enumerate(VARS):
     names[i] = ctx.kernel_name(i)
 os.environ.pop("PBGPU_KERNEL", None)
 os.environ.pop("PBGPU_VP_WGT", None)
+os.environ.pop("PBGPU_VP_POOL", None)
 bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(NBUF)]
 ctx.set_timing(ctx.TIMING_LAUNCH)
 t0 = time.perf_counter()
