@@ -180,8 +180,6 @@ struct pb_kargs
     uint2 *vp_pt;
     const uint2 *lcg48i;    // lcg48i[c] = L^(-48 c), c < PB_VP_NCI
     const uint4 *m16;       // chunk byte masks by plo + phi (PB_VL_NMASK rows: bytes [plo, phi))
-    uint32_t vp_wgt;        // pb_vpage_kernel's threads per workgroup: 256 (4 pages) or 512 (8)
-    uint32_t vp_pool;       // 1: pb_vpool_kernel (the four pages' frame setup by one wave)
 };
 // pb_vpage_kernel: page-relative byte u = start - page start + PB_VP_BIAS (frames < 4 KiB start
 // after the previous page's start), 16-B chunk indices u >> 4 < PB_VP_NCI

@@ -120,8 +120,6 @@ struct pb_opts
                                   // land in registered UMEM by strided DMA instead of the scatter kernel
                                   // (off by default: 1500 B read 56 vs 52 GB/s landing alone on one box,
                                   // 43 vs 49 GB/s in bench.py's build + land on another)
-    uint32_t vp_wgt = 0;       // PBGPU_VP_WGT=512: pb_vpage_kernel with 8 pages per workgroup
-    bool vp_pool = false;      // PBGPU_VP_POOL=1: pb_vpool_kernel (pooled frame setup)
     uint32_t vp_pages_pct = 0; // PBGPU_VP_PAGES_PCT: pb_vpage_kernel's grid as a percentage of the
                                // expected pages (tests: a short grid, so waves take several pages)
 };
@@ -182,8 +180,6 @@ pb_opts read_opts()
     o.vp_pages_pct = opt_u32("PBGPU_VP_PAGES_PCT");
     if (getenv("PBGPU_LAND_DMA_MIN"))
         o.land_dma_min = (uint32_t)atoi(getenv("PBGPU_LAND_DMA_MIN"));
-    o.vp_wgt = opt_u32("PBGPU_VP_WGT") == 512 ? 512u : 256u;
-    o.vp_pool = opt_is("PBGPU_VP_POOL", "1");
     if (opt_u32("PBGPU_ALLOC_CHUNK_MB"))
         o.alloc_chunk_mb = opt_u32("PBGPU_ALLOC_CHUNK_MB");
     return o;
@@ -1369,8 +1365,6 @@ int pbgpu_load_sequence(pbgpu_ctx *ctx, uint16_t seq_idx, const pb_sequence_t *s
                     K.vl = 0;
                     K.vp = 1;
                     K.vp_nfp = nfp;
-                    K.vp_wgt = O.vp_pool ? 256u : O.vp_wgt;
-                    K.vp_pool = O.vp_pool ? 1u : 0u;
                 }
             }
             if (fst_ok)
@@ -1873,7 +1867,7 @@ static int build_impl(pbgpu_ctx *ctx, uint16_t seq_idx, uint64_t first_iter, uin
                 if (S.opt.vp_pages_pct)
                     pages_est = pages_est * S.opt.vp_pages_pct / 100 + 1;
                 const uint64_t pages = pages_est < pages_max ? pages_est : pages_max;
-                const uint64_t ppg = 8ull * (K.vp_wgt == 512 ? 8u : 4u); // pages per group of 8 workgroups
+                const uint64_t ppg = 32; // pages per group of 8 workgroups (4 per workgroup)
                 if ((pages + ppg - 1) / ppg * 8 > 0x7FFFFFFFull)
                     return PBGPU_ENOSPC;
                 K.vp_grid = (uint32_t)((pages + ppg - 1) / ppg * 8);
@@ -2736,8 +2730,8 @@ int pbgpu_kernel_name(pbgpu_ctx *ctx, uint16_t seq_idx, char *buf, size_t n)
         return PBGPU_ENOENT;
     const pb_kargs &K = S.K;
     if (K.vp)
-        snprintf(buf, n, "%s<%u, %u> (after pb_vrec_kernel<%u, %u>)", K.vp_pool ? "pb_vpool_kernel" : "pb_vpage_kernel",
-                 K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u, K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
+        snprintf(buf, n, "pb_vpage_kernel<%u, %u> (after pb_vrec_kernel<%u, %u>)", K.hl,
+                 (K.flags & PBK_L4_CSUM) ? 1u : 0u, K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
     else if (K.vl)
         snprintf(buf, n, "pb_vline_kernel<%u, %u>", K.hl, (K.flags & PBK_L4_CSUM) ? 1u : 0u);
     else if (K.fst_g)

@@ -2911,10 +2911,13 @@ __global__ __launch_bounds__(PB_WG) void pb_vrec_kernel(pb_kargs K)
 //    payload's byte mask; four 1-KiB store instructions (the stream's last chunk zero-padded).
 // Each workgroup's count record is {frames starting in its pages, their page bytes}; pages past the
 // stream (the grid covers the longest possible one) record zeros.
-template <int HL, bool L4, int WGT = PB_WG>
-__global__ __launch_bounds__(WGT) void pb_vpage_kernel(pb_kargs K)
+// (Measured and removed, round 6: 512-thread workgroups of 8 pages, 7.24 vs 6.89 ms; the four
+// pages' frame setup pooled into wave 0 before a workgroup barrier, 7.59 vs 6.93 ms, commit
+// "Pooled-setup page kernel"; profiles/r06/vpage/.)
+template <int HL, bool L4>
+__global__ __launch_bounds__(PB_WG) void pb_vpage_kernel(pb_kargs K)
 {
-    constexpr uint32_t NW = WGT / 64; // pages (waves) per workgroup
+    constexpr uint32_t NW = PB_WG / 64; // pages (waves) per workgroup
     constexpr uint32_t NSP = (15 + HL + 15) / 16; // chunks a frame's header can touch
     constexpr uint32_t NHW = (HL + 6) / 4;       // image dwords written (pb_vline_kernel)
     static_assert(3 + NHW <= 4 * NSP, "image slot");
@@ -3075,196 +3078,6 @@ __global__ __launch_bounds__(WGT) void pb_vpage_kernel(pb_kargs K)
         for (uint32_t w = 0; w < NW; ++w)
             fr += s_cnt[w].x, by += s_cnt[w].y;
         pb_count_at(K, b, pb_xcd_region(b, gridDim.x), fr, by);
-    }
-}
-
-// The page kernel with the frame setup pooled per workgroup (PBGPU_VP_POOL=1): wave 0 sets up the
-// frames of all four pages of its workgroup, 16 lanes per page (a DPP row each), 16 frames per
-// page per pass, so a page of ~6 frames no longer costs a whole wave-pass of header work; after one
-// workgroup barrier each wave builds and stores its own page as pb_vpage_kernel does.
-template <int HL, bool L4>
-__global__ __launch_bounds__(PB_WG) void pb_vpool_kernel(pb_kargs K)
-{
-    constexpr uint32_t NSP = (15 + HL + 15) / 16;
-    constexpr uint32_t NHW = (HL + 6) / 4;
-    static_assert(3 + NHW <= 4 * NSP, "image slot");
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-    const uint32_t NFP = K.vp_nfp;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    pb_u32x4 *const s_m16 = reinterpret_cast<pb_u32x4 *>(s_dyn);
-    uint2 *const s_pg = reinterpret_cast<uint2 *>(s_m16 + PB_VL_NMASK); // per page {bytes, -}
-    uint8_t *const base = reinterpret_cast<uint8_t *>(s_pg + 4);
-    const size_t per = PB_VP_WAVE_LDS(NFP, NSP);
-    auto rec_of = [&](uint32_t g) { return reinterpret_cast<pb_u32x4 *>(base + g * per); };
-    auto img_of = [&](uint32_t g) { return rec_of(g) + NFP; };
-    auto mark_of = [&](uint32_t g) { return reinterpret_cast<uint32_t *>(img_of(g) + NFP * NSP + 1); };
-
-    const uint32_t b = blockIdx.x;
-    const uint32_t g = lane >> 4, j = lane & 15u; // wave 0: page g's setup lane j
-    const uint64_t c_w0 = ((b >> 3) * 4u + wv) * 8u + (b & 7u);
-    const uint64_t c_g0 = ((b >> 3) * 4u + g) * 8u + (b & 7u);
-    const uint64_t stride = 4ull * gridDim.x;
-    const uint64_t total = K.offsets_w[K.n_frames];
-    uint2 tm = make_uint2(0u, 0u), rg1 = make_uint2(0u, 0u);
-    uint4 m16row = make_uint4(0u, 0u, 0u, 0u);
-    if (wv == 0)
-    {
-        tm = lane < 16u ? K.jump[PB_JNEG - (lane + HL)] : K.lcg48i[lane < 32u ? lane - 16u : (lane - 32u) << 4];
-        rg1 = (K.flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
-        if (lane < PB_VL_NMASK)
-            m16row = K.m16[lane];
-    }
-    uint32_t frames = 0, bytes = 0; // wave 0, lane j == 0 of each group: its page's counts
-    for (uint32_t rr = 0; ((c_w0 - wv * 8u + (uint64_t)rr * stride) << 12) < total; ++rr)
-    {
-        if (rr)
-            __syncthreads(); // the previous round's page reads before this round's setup writes
-        if (wv == 0)
-        {
-            const uint64_t c = c_g0 + (uint64_t)rr * stride;
-            const bool pgv = (c << 12) < total;
-            const uint2 e = pgv ? K.vp_pt[c] : make_uint2(0u, 0u);
-            pb_u32x4 *const s_rec = rec_of(g);
-            pb_u32x4 *const s_img = img_of(g);
-            uint32_t *const s_mark = mark_of(g);
-            reinterpret_cast<pb_u32x4 *>(s_mark)[j] = pb_u32x4{0u, 0u, 0u, 0u};
-            if (lane < PB_VL_NMASK)
-                s_m16[lane] = pb_u32x4{m16row.x, m16row.y, m16row.z, m16row.w};
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint32_t carry = 0, nf = 0;
-            bool done = !pgv;
-            for (uint32_t k = 0; k * 16u < NFP; ++k)
-            {
-                const uint64_t f = (uint64_t)e.x + 16u * k + j;
-                const bool fv = !done && f < K.n_frames;
-                const uint2 r = fv ? K.vp_rec[f] : make_uint2(0u, 0u);
-                const uint32_t fl = r.y >> 16;
-                uint32_t inc = fl; // inclusive scan within the 16-lane row (the page's lanes)
-                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x111, 0xF, 0xF, true);
-                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x112, 0xF, 0xF, true);
-                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x114, 0xF, 0xF, true);
-                inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x118, 0xF, 0xF, true);
-                const int32_t st = (int32_t)e.y + (int32_t)(carry + inc - fl);
-                const bool inp = fv && st < 4096;
-                const uint64_t bal = __ballot(inp);
-                const uint32_t slot = 16u * k + j;
-                const uint32_t u = (uint32_t)(st + (int32_t)PB_VP_BIAS);
-                const uint32_t s0 = u & 15u, cs = u >> 4;
-                const uint32_t l1 = s0 << 2, l2 = (16u + (cs & 15u)) << 2, l3 = (32u + ((cs >> 4) & 31u)) << 2;
-                const uint32_t m1a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l1, (int)tm.x);
-                const uint32_t m1c = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l1, (int)tm.y);
-                const uint32_t m2a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l2, (int)tm.x);
-                const uint32_t m2c = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l2, (int)tm.y);
-                const uint32_t m3a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l3, (int)tm.x);
-                const uint32_t m3c = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l3, (int)tm.y);
-                if (inp)
-                {
-                    const uint32_t s = r.x;
-                    const uint32_t r0 = pb_rand_r(s);
-                    uint32_t d[16];
-                    (void)pb_header(K, r0, fl - HL, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
-                    const uint32_t z = pb_mad24v(pb_mad24v(pb_mad24v(s, m1a, m1c), m2a, m2c), m3a, m3c);
-                    s_rec[slot] = pb_u32x4{cs, u + HL, u + fl, z};
-                    const uint32_t q = s0 >> 2, sh = s0 & 3u;
-                    uint32_t *const img32 = reinterpret_cast<uint32_t *>(s_img + slot * NSP) + q;
-#pragma unroll
-                    for (uint32_t w = 0; w < NHW; ++w)
-                    {
-                        const uint32_t lo = w > 0 ? d[w - 1] : 0u, hi = d[w];
-                        img32[w] = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
-                    }
-                    if (L4)
-                    {
-                        uint8_t *const cb =
-                            reinterpret_cast<uint8_t *>(s_img + slot * NSP) + s0 + 4u * K.csum_dw + 2u * K.csum_hi;
-                        cb[0] = (uint8_t)r.y;
-                        cb[1] = (uint8_t)(r.y >> 8);
-                    }
-                    const uint32_t k0 = st <= 0 ? 0u : ((uint32_t)st + 15u) >> 4;
-                    if (k0 < 256u)
-                        reinterpret_cast<uint8_t *>(s_mark)[((k0 & 63u) << 2) + (k0 >> 6)] = 1u;
-                }
-                nf += (uint32_t)__popcll(bal & (0xFFFFull << (16u * g)));
-                carry += (uint32_t)__shfl(inc, (int)(lane | 15u), 64);
-                done = done || !((bal >> (16u * g + 15u)) & 1u); // the page's last lane ended it
-                if (__ballot(!done) == 0)
-                    break;
-            }
-            if (j == 0 && pgv)
-            {
-                s_img[nf * NSP] = pb_u32x4{0u, 0u, 0u, 0u};
-                const uint32_t pbytes = (uint32_t)min((uint64_t)4096, total - (c << 12));
-                s_pg[g] = make_uint2(pbytes, 0u);
-                bytes += pbytes;
-                frames += nf - ((int32_t)e.y < 0 ? 1u : 0u);
-            }
-        }
-        __syncthreads();
-        const uint64_t c = c_w0 + (uint64_t)rr * stride;
-        if ((c << 12) < total)
-        {
-            // the lane's chunk states L^(48 ci) (L1 hits; loaded here, not held through the setup)
-            uint2 lc[4];
-#pragma unroll
-            for (uint32_t i = 0; i < 4; ++i)
-                lc[i] = K.lcg48[PB_VP_BIAS / 16u + 64u * i + lane];
-            const pb_u32x4 *const s_rec = rec_of(wv);
-            const pb_u32x4 *const s_img = img_of(wv);
-            const uint32_t mk = mark_of(wv)[lane];
-            const uint32_t nch = (s_pg[wv].x + 15u) >> 4;
-            uint8_t *const gout = K.out + (c << 12) + (lane << 4);
-            uint32_t pre = 0;
-            pb_u32x4 v[4];
-#pragma unroll
-            for (uint32_t i = 0; i < 4; ++i)
-            {
-                const uint64_t B = __ballot(((mk >> (8u * i)) & 0xFFu) != 0u);
-                const uint32_t below =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
-                const uint32_t fi = pre + below + (uint32_t)((B >> lane) & 1u) - 1u;
-                pre += (uint32_t)__popcll(B);
-                const pb_u32x4 rc = s_rec[fi];
-                const uint32_t ci = PB_VP_BIAS / 16u + 64u * i + lane;
-                const uint32_t m = ci - rc[0];
-                const uint32_t x = pb_mad24v(rc[3], lc[i].x, lc[i].y);
-                const int32_t pb = (int32_t)(ci << 4);
-                const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
-                const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
-                const pb_u32x4 h = s_img[fi * NSP + min(m, NSP)];
-                uint32_t o0, o1, o2, o3;
-                pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
-                const pb_u32x4 mm = s_m16[plo + phi];
-                v[i] = pb_u32x4{(o0 & mm[0]) | (h[0] & ~mm[0]), (o1 & mm[1]) | (h[1] & ~mm[1]),
-                                (o2 & mm[2]) | (h[2] & ~mm[2]), (o3 & mm[3]) | (h[3] & ~mm[3])};
-            }
-            if (nch == 256u)
-            {
-#pragma unroll
-                for (uint32_t i = 0; i < 4; ++i)
-                    pb_st16_nt(gout + (i << 10), v[i]);
-            }
-            else
-            {
-#pragma unroll
-                for (uint32_t i = 0; i < 4; ++i)
-                    if (64u * i + lane < nch)
-                        pb_st16_nt(gout + (i << 10), v[i]);
-            }
-        }
-    }
-    if (wv == 0)
-    {
-        // the four pages' counts (lanes 0, 16, 32, 48) into the workgroup's record
-        uint32_t fr = frames, by = bytes;
-        fr += __shfl_xor(fr, 16, 64);
-        by += __shfl_xor(by, 16, 64);
-        fr += __shfl_xor(fr, 32, 64);
-        by += __shfl_xor(by, 32, 64);
-        if (lane == 0)
-            pb_count_at(K, b, pb_xcd_region(b, gridDim.x), fr, by);
     }
 }
 
@@ -3652,18 +3465,12 @@ extern "C" hipError_t pbk_launch_build(const pb_kargs *K, hipStream_t st)
         const uint32_t rgrid = (uint32_t)((K->n_frames + PB_WG - 1) / PB_WG);
         const bool l4 = (K->flags & PBK_L4_CSUM) != 0;
         const uint32_t nsp = K->hl == 54 ? 5u : 4u;
-        const uint32_t nw = K->vp_wgt == 512 ? 8u : 4u;
-        const size_t lds = PB_VP_LDS(K->vp_nfp, nsp, nw);
+        const size_t lds = PB_VP_LDS(K->vp_nfp, nsp, 4);
 #define PB_VP(HH, LL)                                                                                       \
     do                                                                                                      \
     {                                                                                                       \
         hipLaunchKernelGGL((pb_vrec_kernel<HH, LL>), dim3(rgrid), dim3(PB_WG), 0, st, *K);                  \
-        if (K->vp_pool)                                                                                     \
-            hipLaunchKernelGGL((pb_vpool_kernel<HH, LL>), dim3(K->vp_grid), dim3(PB_WG), lds, st, *K);      \
-        else if (nw == 8)                                                                                   \
-            hipLaunchKernelGGL((pb_vpage_kernel<HH, LL, 512>), dim3(K->vp_grid), dim3(512), lds, st, *K);   \
-        else                                                                                                \
-            hipLaunchKernelGGL((pb_vpage_kernel<HH, LL>), dim3(K->vp_grid), dim3(PB_WG), lds, st, *K);      \
+        hipLaunchKernelGGL((pb_vpage_kernel<HH, LL>), dim3(K->vp_grid), dim3(PB_WG), lds, st, *K);          \
     } while (0)
         if (K->hl == 54)
         {

@@ -22,21 +22,14 @@ ctx = GpuContext(0)
 seq = Sequence.from_config(pc.get("c3_udp_var"))
 names = {}
 for i, v in enumerate(VARS):
-    # a variant is a PBGPU_KERNEL value, optionally with PBGPU_VP_WGT after a colon (vpage:512), or
-    # vpage:pool for PBGPU_VP_POOL=1
-    kern, _, wgt = v.partition(":")
-    pool = "1" if wgt == "pool" else ""
-    wgt = "" if pool else wgt
-    for key, val in (("PBGPU_KERNEL", kern), ("PBGPU_VP_WGT", wgt), ("PBGPU_VP_POOL", pool)):
-        if val:
-            os.environ[key] = val
-        else:
-            os.environ.pop(key, None)
+    # (the round-6 forms vpage:512 and vpage:pool selected kernels since removed)
+    if v:
+        os.environ["PBGPU_KERNEL"] = v
+    else:
+        os.environ.pop("PBGPU_KERNEL", None)
     ctx.load_sequence(i, seq, pc.SEED_BASE)
     names[i] = ctx.kernel_name(i)
 os.environ.pop("PBGPU_KERNEL", None)
-os.environ.pop("PBGPU_VP_WGT", None)
-os.environ.pop("PBGPU_VP_POOL", None)
 bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(NBUF)]
 ctx.set_timing(ctx.TIMING_LAUNCH)
 t0 = time.perf_counter()

@@ -323,15 +323,12 @@ VL_RANGES = [(32, 33), (32, 40), (32, 200), (60, 1500), (64, 1500), (1400, 1500)
 @pytest.mark.parametrize("lo,hi", VL_RANGES)
 @pytest.mark.parametrize("proto", ["udp", "tcp", "icmp"])
 @pytest.mark.parametrize("csum", [True, False])
-@pytest.mark.parametrize("kernel", ["vpage", "vpool", "vline"])
+@pytest.mark.parametrize("kernel", ["vpage", "vline"])
 def test_vline_variable_lengths(ctx, monkeypatch, proto, lo, hi, csum, kernel):
-    """pb_vline_kernel (the default), pb_vpage_kernel (PBGPU_KERNEL=vpage: up to 57 frames per
-    page at 74 B, frames up to 4 KiB starting up to a page before the page) and its pooled-setup
-    form pb_vpool_kernel (PBGPU_VP_POOL=1: 16 frames per page per pass, up to 4 passes)."""
-    if kernel in ("vpage", "vpool"):
+    """pb_vline_kernel (the default) and pb_vpage_kernel (PBGPU_KERNEL=vpage: up to 57 frames per
+    page at 74 B, frames up to 4 KiB starting up to a page before the page)."""
+    if kernel == "vpage":
         monkeypatch.setenv("PBGPU_KERNEL", "vpage")
-    if kernel == "vpool":
-        monkeypatch.setenv("PBGPU_VP_POOL", "1")
     hl = 54 if proto == "tcp" else 42
     cfg = _fst_cfg(proto, hl + 100, csum)
     cfg["payloads"] = [{"length": {"min": lo, "max": hi}}]
@@ -406,19 +403,13 @@ def test_vline_matches_vstage_at_size(ctx, monkeypatch):
 
 
 @pytest.mark.parametrize("pct", ["1", "30", "100"])
-@pytest.mark.parametrize("wgt", ["256", "512", "pool"])
-def test_vpage_short_grid_waves_take_several_pages(ctx, monkeypatch, pct, wgt):
+def test_vpage_short_grid_waves_take_several_pages(ctx, monkeypatch, pct):
     """pb_vpage_kernel's grid covers the expected stream; a longer one is built by the same waves
-    in later rounds (PBGPU_VP_PAGES_PCT shrinks the grid so every wave loops), at 4 and 8 pages
-    per workgroup (PBGPU_VP_WGT): bit-exact."""
+    in later rounds (PBGPU_VP_PAGES_PCT shrinks the grid so every wave loops): bit-exact."""
     monkeypatch.setenv("PBGPU_KERNEL", "vpage")
     monkeypatch.setenv("PBGPU_VP_PAGES_PCT", pct)
-    if wgt == "pool":
-        monkeypatch.setenv("PBGPU_VP_POOL", "1")
-    else:
-        monkeypatch.setenv("PBGPU_VP_WGT", wgt)
     for lo, hi in ((32, 33), (64, 1500), (3000, 4042)):
         cfg = pc.get("c3_udp_var")
         cfg["payloads"] = [{"length": {"min": lo, "max": hi}}]
         kern = _check(ctx, cfg, 99, 30011)
-        assert kern.startswith("pb_vpool_kernel<" if wgt == "pool" else "pb_vpage_kernel<"), kern
+        assert kern.startswith("pb_vpage_kernel<"), kern
