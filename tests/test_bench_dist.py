@@ -8,6 +8,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -128,8 +129,7 @@ def _worker(rank, world, port, names, q):
     q.put((rank, ctx.builds, ctx.batches, res["counters"], res["wall_s"], res["kernels"], res["packets_per_step"]))
 
 
-def _run(names):
-    world = 2
+def _run(names, world=2):
     c = mp.get_context("spawn")
     q = c.Queue()
     port = _free_port()
@@ -143,8 +143,8 @@ def _run(names):
     return res
 
 
-def _check(res, names):
-    world, steps, warmup, n = 2, 3, 2, 1000
+def _check(res, names, world=2):
+    steps, warmup, n = 3, 2, 1000
     nseq = len(names)
     seen = set()
     walls = []
@@ -164,7 +164,8 @@ def _check(res, names):
         walls.append(wall)
         if nseq > 1:
             assert batches == warmup + steps + 2 and kernels[0].startswith("pb_batch_kernel")
-    assert walls[0] == walls[1] and walls[0] >= 0.3  # MAX over ranks: the slow rank's wall
+    assert len(set(walls)) == 1 and walls[0] >= 0.3  # MAX over ranks: the slow rank's wall
+    assert len(seen) == nseq * world * (warmup + steps + 2)
 
 
 def test_bench_world2_one_sequence():
@@ -175,3 +176,11 @@ def test_bench_world2_one_sequence():
 def test_bench_world2_mix_batch():
     names = ["c2_udp_64", "c4_tcp_syn", "c5_icmp_echo"]
     _check(_run(names), names)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_bench_more_ranks(world):
+    """The driver's 4- and 8-GPU runs rehearsed on CPU: every rank's iteration ranges disjoint,
+    counters all-reduced to world x steps x n, the wall the slowest rank's."""
+    names = ["c2_udp_64", "c4_tcp_syn", "c5_icmp_echo"] if world == 4 else ["c2_udp_64"]
+    _check(_run(names, world), names, world)

@@ -1,4 +1,4 @@
-"""Multi-rank path on CPU (gloo, world size 2): shard ranges partition the
+"""Multi-rank path on CPU (gloo, world sizes 2 and 8): shard ranges partition the
 iteration space, per-rank builds concatenate to the single-rank build, and the
 counter all-reduce gives the global totals.  The per-rank builder here is the
 oracle (no GPU in this container); the GPU version of the concatenation
@@ -61,12 +61,13 @@ def _worker(rank, world, port, q):
     q.put((rank, gp[0], gb[0], hashlib.sha256(b"".join(objs)).hexdigest()))
 
 
-def test_gloo_world2_shards_concatenate_and_counters_reduce():
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_world2_shards_concatenate_and_counters_reduce(world):
+    """world 2, and the driver's 8-rank case rehearsed (601 iterations: ragged shards)"""
     import oracle_binding as ob
     import pb_configs as pc
     from pbgpu import Sequence
 
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
