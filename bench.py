@@ -212,25 +212,26 @@ def run_configs(ctx, names, n_pkts, steps, warmup, rank, world, dist, local, ram
             "per_seq_bytes_per_step": [x // steps for x in db], "kernels": kernels}
 
 
-def d2h_rate(ctx, seq_idx, n_pkts):
-    """Build + land into 4 KiB UMEM slots in pinned host memory (af_xdp.c:200-214)."""
+def d2h_rate(ctx, seq_idx, n_pkts, slot=4096):
+    """Build + land into UMEM slots in pinned host memory: 4 KiB (af_xdp.c:200-214), or the
+    smaller slots of --umemslot (64 B: back to back, written whole)."""
     n = min(n_pkts, 1 << 18)
-    umem = np.zeros(n * 4096, dtype=np.uint8)
+    umem = np.zeros(n * slot, dtype=np.uint8)
     ctx.lib.pbgpu_host_register(ctx.h, umem.ctypes.data, umem.nbytes)
     fb = ctx.alloc_frames(*ctx.build_size(seq_idx, n))
     ctx.build(seq_idx, 0, n, fb)
-    fb.to_umem(umem, 4096, 0, n)
+    fb.to_umem(umem, slot, 0, n)
     t0 = time.perf_counter()
     reps = 5
     for r in range(reps):
         ctx.build(seq_idx, r * n, n, fb)
-        fb.to_umem(umem, 4096, 0, n)
+        fb.to_umem(umem, slot, 0, n)
     dt = (time.perf_counter() - t0) / reps
     frame_bytes = fb.total_bytes()
     fb.free()
     ctx.kernel_time()
     ctx.lib.pbgpu_host_unregister(ctx.h, umem.ctypes.data)
-    return {"packets": n, "mpps": n / dt / 1e6, "ms_per_batch": dt * 1e3, "slot": 4096,
+    return {"packets": n, "mpps": n / dt / 1e6, "ms_per_batch": dt * 1e3, "slot": slot,
             "frame_gbps": frame_bytes / dt / 1e9}
 
 
@@ -351,6 +352,7 @@ def main():
             ctx.load_sequence(0, Sequence.from_config(pc.get("c2_udp_64")), pc.SEED_BASE)
             ctx.load_sequence(1, Sequence.from_config(pc.get("c2_udp_1500")), pc.SEED_BASE)
             extra["d2h_umem_64B"] = d2h_rate(ctx, 0, a.packets)
+            extra["d2h_umem_64B_slot64"] = d2h_rate(ctx, 0, a.packets, 64)
             extra["d2h_umem_1500B"] = d2h_rate(ctx, 1, a.packets)
     if not a.no_variants and a.config != "c2_udp_64" and a.config != "c5_mix" and rank == 0:
         # the configured sequence (still loaded at index 0) landed into UMEM slots

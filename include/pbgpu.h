@@ -133,6 +133,11 @@ int pbgpu_copy_offsets(pbgpu_ctx *ctx, const pbgpu_frames *frames, uint64_t *hos
 /* UMEM landing (af_xdp.c:200-214 geometry): frame first_frame + j lands at
  * umem + (first_slot + j) * slot_stride; lens_out[j] = its length.  `umem`
  * may be any host pointer; pbgpu_host_register() it first for full speed.
+ * Nothing past a frame in its slot is written, except in a tight slot (fixed
+ * length, slot_stride no longer than the frame rounded up to 64 B: 64-B slots
+ * for 60- or 64-B frames), which registered UMEM receives whole, the bytes past
+ * the frame unspecified: back-to-back slots then cross the host link as
+ * contiguous writes.
  * Runs on the context's landing stream after the build of `frames` only, so a
  * build of another buffer queued meanwhile overlaps it (double buffering);
  * returns when the frames are in place.  A frame longer than slot_stride is

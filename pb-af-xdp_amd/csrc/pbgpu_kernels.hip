@@ -3239,26 +3239,33 @@ __global__ __launch_bounds__(64) void pb_scatter_slots(const uint8_t *src, const
         reinterpret_cast<uint8_t *>(d + i)[threadIdx.x] = s[4 * i + threadIdx.x];
 }
 
-// fixed-length frames -> slots: thread (f, i) stores dword i of frame f (f = gid / dpf)
-// at dst + f * stride; straight over the host link when dst is mapped UMEM
-// (af_xdp.c:211-214 geometry: one frame per 4 KiB slot)
-__global__ __launch_bounds__(256) void pb_scatter_fixed(const uint8_t *src, uint32_t flen, uint32_t dpf, uint64_t n_dw,
-                                                        uint8_t *dst, uint32_t stride)
+// fixed-length frames -> slots: thread (f, i) stores dword i of slot f (f = gid / dpf) at
+// dst + f * stride; straight over the host link when dst is mapped UMEM (af_xdp.c:211-214
+// geometry: one frame per 4 KiB slot).  wlen bytes of each slot are written: the frame's flen,
+// or the whole slot (wlen = stride, a multiple of 4) when the slot is tight, the frame's bytes
+// followed by the packed stream's next ones (zeros past src_lim, the source bytes readable):
+// contiguous slots then leave as contiguous host-link writes
+__global__ __launch_bounds__(256) void pb_scatter_fixed(const uint8_t *src, uint32_t flen, uint32_t wlen, uint32_t dpf,
+                                                        uint64_t n_dw, uint64_t src_lim, uint8_t *dst, uint32_t stride)
 {
     const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= n_dw)
         return;
     const uint64_t f = g / dpf;
     const uint32_t i = (uint32_t)(g - f * dpf);
-    const uint8_t *s = src + f * flen + 4 * i;
+    const uint64_t o = f * flen + 4 * i;
+    const uint8_t *s = src + o;
     const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)s & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
-    const uint32_t v = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+    // the frame's own dwords read at most 3 bytes past it (inside the buffer's 16-B tail pad);
+    // a filler dword is read only while the stream has the bytes
+    const bool rd = 4 * i < flen || o + 8 <= src_lim;
+    const uint32_t v = rd ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : 0u;
     uint8_t *d = dst + f * stride + 4 * i;
-    if (4 * i + 4 <= flen)
+    if (4 * i + 4 <= wlen)
         *reinterpret_cast<uint32_t *>(d) = v;
     else
-        for (uint32_t b = 0; 4 * i + b < flen; ++b)
+        for (uint32_t b = 0; 4 * i + b < wlen; ++b)
             d[b] = (uint8_t)(v >> (8 * b));
 }
 
@@ -3695,13 +3702,13 @@ extern "C" hipError_t pbk_launch_lengths(const pb_kargs *K, unsigned long long *
     return hipGetLastError();
 }
 
-extern "C" hipError_t pbk_launch_scatter_fixed(const uint8_t *src, uint32_t flen, uint32_t n, uint8_t *dst,
-                                               uint32_t stride, hipStream_t st)
+extern "C" hipError_t pbk_launch_scatter_fixed(const uint8_t *src, uint32_t flen, uint32_t wlen, uint32_t n,
+                                               uint64_t src_lim, uint8_t *dst, uint32_t stride, hipStream_t st)
 {
-    const uint32_t dpf = (flen + 3) / 4;
+    const uint32_t dpf = (wlen + 3) / 4;
     const uint64_t n_dw = (uint64_t)n * dpf;
-    hipLaunchKernelGGL(pb_scatter_fixed, dim3((uint32_t)((n_dw + 255) / 256)), dim3(256), 0, st, src, flen, dpf, n_dw,
-                       dst, stride);
+    hipLaunchKernelGGL(pb_scatter_fixed, dim3((uint32_t)((n_dw + 255) / 256)), dim3(256), 0, st, src, flen, wlen, dpf,
+                       n_dw, src_lim, dst, stride);
     return hipGetLastError();
 }
 

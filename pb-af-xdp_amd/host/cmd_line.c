@@ -35,6 +35,7 @@ enum
     OPT_TX,
     OPT_VERYRANDOM,
     OPT_UMEMFRAMES,
+    OPT_UMEMSLOT,
 };
 
 static const struct option af_xdp_opts[] = {
@@ -55,6 +56,7 @@ static const struct option af_xdp_opts[] = {
     {"tx", required_argument, NULL, OPT_TX},
     {"veryrandom", no_argument, NULL, OPT_VERYRANDOM},
     {"umemframes", required_argument, NULL, OPT_UMEMFRAMES},
+    {"umemslot", required_argument, NULL, OPT_UMEMSLOT},
     {NULL, 0, NULL, 0},
 };
 
@@ -129,6 +131,9 @@ void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *c, int argc, char **argv)
         case OPT_UMEMFRAMES:
             c->umem_frames = (uint32_t)strtoul(optarg, NULL, 0);
             break;
+        case OPT_UMEMSLOT:
+            c->umem_slot = (uint32_t)strtoul(optarg, NULL, 0);
+            break;
         default:
             break;
         }
@@ -145,6 +150,13 @@ int pb_af_xdp_setup(const struct cmd_line_af_xdp *c, int verbose)
     if (c->umem_frames < 64 || c->umem_frames > (1u << 20) || (c->umem_frames & (c->umem_frames - 1)))
     {
         fprintf(stderr, "--umemframes must be a power of two from 64 to 1048576.\n");
+        return -EINVAL;
+    }
+    if (c->umem_slot &&
+        (c->umem_slot < 64 || c->umem_slot > 4096 || (c->umem_slot & (c->umem_slot - 1)) ||
+         (uint64_t)c->umem_frames * (4096u / c->umem_slot) > (1u << 22)))
+    {
+        fprintf(stderr, "--umemslot must be a power of two from 64 to 4096, at most 2^22 slots per UMEM.\n");
         return -EINVAL;
     }
     if (c->batch_set && c->batch_size == 0)

@@ -36,6 +36,9 @@ typedef struct cmd_line_af_xdp
     int very_random;     /* --veryrandom: draw it with getrandom() (VERY_RANDOM, sequence.h:36) */
     int batch_set;       /* --batchsize given: TX descriptors per reserve / submit (else one landed chunk) */
     uint32_t umem_frames; /* --umemframes N: UMEM slots per socket (NUM_FRAMES = 4096, af_xdp.h:23; a power of two) */
+    uint32_t umem_slot;   /* --umemslot S: bytes per frame slot (FRAME_SIZE = 4096, af_xdp.h:24, when 0): the UMEM of
+                             umem_frames 4-KiB chunks is cut into slots of S bytes (a power of two, 64..4096), so
+                             S = 64 lands 64 frames per chunk, contiguously */
 } cmd_line_af_xdp_t;
 
 void parse_cmd_line_af_xdp(struct cmd_line_af_xdp *cmd_af_xdp, int argc, char **argv);
@@ -44,7 +47,8 @@ void cmd_line_af_xdp_defaults(struct cmd_line_af_xdp *cmd_af_xdp);
 /* setup_af_xdp_variables() (af_xdp.c:289-365): the reference's verbose lines, and the
  * checks this build adds: --skb (SKB / generic XDP mode, xdp_flags = XDP_FLAGS_SKB_MODE)
  * runs the socket in copy mode, so --skb with --zerocopy is refused; --batchsize 0 is
- * refused; --umemframes must be a power of two in [64, 2^20].  Returns 0, or -EINVAL after
+ * refused; --umemframes must be a power of two in [64, 2^20], --umemslot 0 or a power of two in
+ * [64, 4096] giving at most 2^22 slots.  Returns 0, or -EINVAL after
  * a message on stderr. */
 int pb_af_xdp_setup(const struct cmd_line_af_xdp *cmd_af_xdp, int verbose);
 /* bind flags of a socket (af_xdp.c:291-320): need-wakeup unless --nowakeup;

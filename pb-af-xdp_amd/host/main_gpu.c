@@ -80,7 +80,7 @@ static const struct option common_opts[] = {
     {"seed", required_argument, NULL, O_SECOND_PASS}, {"literal", no_argument, NULL, O_SECOND_PASS},
     {"singlefold", no_argument, NULL, O_SECOND_PASS}, {"pcap", required_argument, NULL, O_SECOND_PASS},
     {"tx", required_argument, NULL, O_SECOND_PASS}, {"veryrandom", no_argument, NULL, O_SECOND_PASS},
-    {"umemframes", required_argument, NULL, O_SECOND_PASS},
+    {"umemframes", required_argument, NULL, O_SECOND_PASS}, {"umemslot", required_argument, NULL, O_SECOND_PASS},
     {NULL, 0, NULL, 0},
 };
 
@@ -178,7 +178,7 @@ static void print_cmd_help(void)
                     "-z --cli => Enables the first sequence/packet override (README.md first-sequence options).\n\n"
                     "AF_XDP: --queue --nowakeup --sharedumem --batchsize --skb --zerocopy --copy\n"
                     "GPU: --gpus N --gpu I --gpubatch K --seed S --veryrandom --literal --singlefold --pcap FILE --tx xsk "
-                    "--umemframes N\n");
+                    "--umemframes N --umemslot S\n");
 }
 
 int main(int argc, char **argv)
@@ -248,11 +248,12 @@ int main(int argc, char **argv)
                 cmd_af_xdp.queue_set, cmd_af_xdp.queue, cmd_af_xdp.no_wake_up, cmd_af_xdp.shared_umem,
                 cmd_af_xdp.batch_size, cmd_af_xdp.skb_mode, cmd_af_xdp.zero_copy, cmd_af_xdp.copy);
         fprintf(stdout,
-                "GPU: gpus=%d gpu=%d gpubatch=%llu seed=%llu literal=%d singlefold=%d pcap=%s tx=%s umemframes=%u\n",
+                "GPU: gpus=%d gpu=%d gpubatch=%llu seed=%llu literal=%d singlefold=%d pcap=%s tx=%s umemframes=%u "
+                "umemslot=%u\n",
                 cmd_af_xdp.gpus, cmd_af_xdp.gpu_first, (unsigned long long)cmd_af_xdp.gpu_batch,
                 (unsigned long long)cmd_af_xdp.seed_base, cmd_af_xdp.literal_payload, cmd_af_xdp.single_fold,
                 cmd_af_xdp.pcap ? cmd_af_xdp.pcap : "(none)", cmd_af_xdp.tx ? cmd_af_xdp.tx : "ring",
-                cmd_af_xdp.umem_frames);
+                cmd_af_xdp.umem_frames, cmd_af_xdp.umem_slot ? cmd_af_xdp.umem_slot : 4096u);
         for (int i = 0; i < seq_cnt; ++i)
             fprintf(stdout, "Sequence #%d: %s -> %s proto %s, %u payload(s)\n", i + 1,
                     cfg->seq[i].ip.src_ip ? cfg->seq[i].ip.src_ip

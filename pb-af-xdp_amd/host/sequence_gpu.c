@@ -335,12 +335,15 @@ static void *gpu_worker(void *p)
     memset(&xsk, 0, sizeof xsk);
     xsk.fd = -1;
     sink_arg_t sink = {w->shard, seq_num};
-    /* this thread's UMEM slots: its own NUM_FRAMES (--umemframes), or its range of the
-     * sequence's shared UMEM */
+    /* this thread's UMEM slots: its own NUM_FRAMES chunks of FRAME_SIZE (--umemframes) cut into
+     * slots of --umemslot bytes (one per chunk by default), or its range of the sequence's
+     * shared UMEM */
     const uint32_t umem_frames = w->cmd.umem_frames ? w->cmd.umem_frames : PB_NUM_FRAMES;
-    const uint32_t nslots = w->shared ? w->shared->slots : umem_frames;
+    const uint32_t slot_sz = w->cmd.umem_slot ? w->cmd.umem_slot : PB_FRAME_SIZE;
+    const uint32_t umem_slots = umem_frames * (PB_FRAME_SIZE / slot_sz);
+    const uint32_t nslots = w->shared ? w->shared->slots : umem_slots;
     const uint32_t slot_base = w->shared ? (uint32_t)w->shard * nslots : 0;
-    const size_t umem_bytes = (size_t)nslots * PB_FRAME_SIZE;
+    const size_t umem_bytes = (size_t)nslots * slot_sz;
     uint16_t *lens = (uint16_t *)calloc(nslots, sizeof(uint16_t));
     int rc;
     if (lens == NULL)
@@ -423,7 +426,7 @@ static void *gpu_worker(void *p)
     if (w->shared)
     {
         umem_base = w->shared->base;
-        umem = umem_base + (size_t)slot_base * PB_FRAME_SIZE;
+        umem = umem_base + (size_t)slot_base * slot_sz;
     }
     else
     {
@@ -461,8 +464,8 @@ static void *gpu_worker(void *p)
             }
         }
         pb_xsk_shared_cq_t *scq = w->shared && w->shared->one_queue ? &w->shared->scq : NULL;
-        rc = pb_xsk_open(&xsk, w->device, q, umem_base, nslots, PB_FRAME_SIZE, bf, shared_fd, slot_base,
-                         w->shared ? umem_frames : nslots, w->cmd.queue_set ? (uint32_t)w->cmd.queue : 0u, scq,
+        rc = pb_xsk_open(&xsk, w->device, q, umem_base, nslots, slot_sz, PB_FRAME_SIZE, bf, shared_fd, slot_base,
+                         w->shared ? umem_slots : nslots, w->cmd.queue_set ? (uint32_t)w->cmd.queue : 0u, scq,
                          (uint32_t)w->shard);
         if (w->shared && w->shard == 0)
         {
@@ -479,8 +482,8 @@ static void *gpu_worker(void *p)
         }
     }
     else if ((rc = w->shared && w->shared->one_queue
-                       ? pb_xsk_loopback_shared(&xsk, umem_base, PB_FRAME_SIZE, &w->shared->scq, (uint32_t)w->shard)
-                       : pb_xsk_loopback(&xsk, umem_base, nslots, PB_FRAME_SIZE)) != 0)
+                       ? pb_xsk_loopback_shared(&xsk, umem_base, slot_sz, &w->shared->scq, (uint32_t)w->shard)
+                       : pb_xsk_loopback(&xsk, umem_base, nslots, slot_sz)) != 0)
     {
         last_error = rc;
         goto out;
@@ -555,10 +558,11 @@ static void *gpu_worker(void *p)
                     n = (uint32_t)(nf - f_issue);
                 if (n > nslots - land_slot) /* the slot ring wraps: a chunk never does */
                     n = nslots - land_slot;
-                if ((rc = B->land(ctx, fr[cur], umem, PB_FRAME_SIZE, land_slot, f_issue, n, lens + land_slot)) != 0)
+                if ((rc = B->land(ctx, fr[cur], umem, slot_sz, land_slot, f_issue, n, lens + land_slot)) != 0)
                 {
-                    fprintf(stderr, "[%d] Error landing frames from GPU %d :: %s.\n", seq_num, w->gpu,
-                            pbgpu_strerror(rc));
+                    fprintf(stderr, "[%d] Error landing frames from GPU %d :: %s%s.\n", seq_num, w->gpu,
+                            pbgpu_strerror(rc),
+                            rc == PBGPU_EINVAL && slot_sz < PB_FRAME_SIZE ? " (frames longer than --umemslot?)" : "");
                     last_error = rc;
                     done = 3;
                     break;
@@ -631,7 +635,7 @@ static void *gpu_worker(void *p)
             }
             if (verbose) /* the slots keep these frames until this thread lands into them again */
                 for (uint32_t i = 0; i < n; ++i)
-                    print_sent(seq_num, (uint32_t)((f0 + i) % fpi), seq, umem + (size_t)(sent_slot + i) * PB_FRAME_SIZE,
+                    print_sent(seq_num, (uint32_t)((f0 + i) % fpi), seq, umem + (size_t)(sent_slot + i) * slot_sz,
                                ln[i]);
             __atomic_add_fetch(&total_pckts[w->seq_idx], n, __ATOMIC_RELAXED);
             my_frames += n;
@@ -765,6 +769,13 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
             return;
         }
     }
+    if (cmd.umem_slot && (cmd.umem_slot < 64 || cmd.umem_slot > PB_FRAME_SIZE || (cmd.umem_slot & (cmd.umem_slot - 1))))
+    {
+        fprintf(stderr, "[%d] --umemslot %u is not a power of two from 64 to %u.\n", seq_cnt + 1, cmd.umem_slot,
+                PB_FRAME_SIZE);
+        last_error = PBGPU_EINVAL;
+        return;
+    }
     const uint16_t idx = seq_cnt++;
     start_time[idx] = time(NULL);
     shared_umem_t *shared = NULL;
@@ -773,13 +784,15 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
         /* one UMEM for the sequence's threads (af_xdp.c:412-428), each its own power-of-two
          * slot range */
         const uint32_t umem_frames = cmd.umem_frames ? cmd.umem_frames : PB_NUM_FRAMES;
-        uint32_t slots = umem_frames;
-        while (slots > 1 && slots * (uint32_t)t_cnt > umem_frames)
+        const uint32_t slot_sz = cmd.umem_slot ? cmd.umem_slot : PB_FRAME_SIZE;
+        const uint32_t umem_slots = umem_frames * (PB_FRAME_SIZE / slot_sz);
+        uint32_t slots = umem_slots;
+        while (slots > 1 && slots * (uint32_t)t_cnt > umem_slots)
             slots >>= 1;
-        if (slots * (uint32_t)t_cnt > umem_frames)
+        if (slots * (uint32_t)t_cnt > umem_slots)
         {
-            fprintf(stderr, "[%d] Too many threads (%d) for one shared UMEM of %u frames.\n", idx + 1, t_cnt,
-                    umem_frames);
+            fprintf(stderr, "[%d] Too many threads (%d) for one shared UMEM of %u slots.\n", idx + 1, t_cnt,
+                    umem_slots);
             last_error = PBGPU_EINVAL;
             return;
         }
@@ -799,7 +812,7 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
         if (cmd.queue_set && t_cnt > 1)
         {
             const int loop = !(cmd.tx && strcmp(cmd.tx, "xsk") == 0);
-            const int src = pb_xsk_scq_init(&shared->scq, (uint32_t)t_cnt, slots, PB_FRAME_SIZE, loop);
+            const int src = pb_xsk_scq_init(&shared->scq, (uint32_t)t_cnt, slots, slot_sz, loop);
             if (src != 0)
             {
                 free(shared->base);

@@ -247,11 +247,15 @@ static int map_ring(int fd, pb_xsk_ring_t *r, const struct xdp_ring_offset *off,
 }
 
 int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, uint32_t n_frames,
-                uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames,
-                uint32_t shared_queue, pb_xsk_shared_cq_t *scq, uint32_t thread)
+                uint32_t frame_size, uint32_t chunk_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base,
+                uint32_t umem_frames, uint32_t shared_queue, pb_xsk_shared_cq_t *scq, uint32_t thread)
 {
+    const uint64_t umem_bytes = (uint64_t)(umem_frames ? umem_frames : n_frames) * frame_size;
+    if (chunk_size == 0)
+        chunk_size = frame_size;
     if (x == NULL || ifname == NULL || umem == NULL || n_frames == 0 || (n_frames & (n_frames - 1)) ||
-        slot_base + n_frames > (umem_frames ? umem_frames : n_frames))
+        slot_base + n_frames > (umem_frames ? umem_frames : n_frames) || frame_size == 0 ||
+        chunk_size % frame_size || umem_bytes % chunk_size)
         return -EINVAL;
     /* xsk_bind: XDP_SHARED_UMEM on the owner's (device, queue) shares its buffer pool and
      * rejects a socket with fill / completion rings of its own: such a socket takes none and
@@ -279,8 +283,8 @@ int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, 
     struct xdp_umem_reg mr;
     memset(&mr, 0, sizeof mr);
     mr.addr = (uint64_t)(uintptr_t)umem;
-    mr.len = (uint64_t)(umem_frames ? umem_frames : n_frames) * frame_size;
-    mr.chunk_size = frame_size;
+    mr.len = umem_bytes;
+    mr.chunk_size = chunk_size;
     int rc = 0;
     const int ring_n = (int)n_frames;
     /* the owner's fill and completion rings cover the whole UMEM when queues share it */

@@ -89,7 +89,7 @@ typedef struct pb_xsk
     int fd;           /* AF_XDP socket, -1 for the loopback */
     uint8_t *umem;    /* n_frames * frame_size, page aligned */
     uint32_t n_frames;
-    uint32_t frame_size;
+    uint32_t frame_size; /* bytes per slot: the descriptors' address stride (--umemslot; FRAME_SIZE by default) */
     pb_xsk_ring_t tx;
     pb_xsk_ring_t cq;
     pb_xsk_ring_t fq;  /* fill ring (the kernel requires one per UMEM; unused for TX) */
@@ -130,7 +130,13 @@ typedef void (*pb_xsk_sink_fn)(void *ctx, const uint8_t *frame, uint32_t len, ui
 uint32_t pb_xsk_loop_consume(pb_xsk_t *x, uint32_t max, pb_xsk_sink_fn sink, void *ctx);
 
 /* AF_XDP socket on (ifname, queue) over the UMEM, TX ring and completion ring
- * of n_frames entries.  bind_flags: XDP_COPY / XDP_ZEROCOPY / XDP_USE_NEED_WAKEUP
+ * of n_frames entries, slots of frame_size bytes.  The UMEM is registered in
+ * chunks of chunk_size bytes (0: frame_size; FRAME_SIZE = 4096 for the
+ * reference's geometry): a slot smaller than its chunk (--umemslot) puts
+ * chunk_size / frame_size frames in each chunk, which the kernel's aligned mode
+ * accepts for TX (a descriptor may start anywhere in its chunk and must not
+ * cross its end); chunk_size must be a multiple of frame_size and divide the
+ * UMEM's bytes.  bind_flags: XDP_COPY / XDP_ZEROCOPY / XDP_USE_NEED_WAKEUP
  * (af_xdp.c:289-330).  shared_fd >= 0: the UMEM is already registered on that
  * socket (--sharedumem, af_xdp.c:412-428): this socket binds with
  * XDP_SHARED_UMEM and its own fill / completion rings, and uses the n_frames
@@ -143,7 +149,7 @@ uint32_t pb_xsk_loop_consume(pb_xsk_t *x, uint32_t max, pb_xsk_sink_fn sink, voi
  * any socket is made.  Returns 0, or -errno (EPERM without CAP_NET_RAW,
  * EAFNOSUPPORT without AF_XDP). */
 int pb_xsk_open(pb_xsk_t *x, const char *ifname, uint32_t queue, uint8_t *umem, uint32_t n_frames,
-                uint32_t frame_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames,
+                uint32_t frame_size, uint32_t chunk_size, uint16_t bind_flags, int shared_fd, uint32_t slot_base, uint32_t umem_frames,
                 uint32_t shared_queue, pb_xsk_shared_cq_t *scq, uint32_t thread);
 void pb_xsk_close(pb_xsk_t *x);
 

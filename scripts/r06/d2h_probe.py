@@ -6,6 +6,8 @@ built once), into pinned registered host memory:
               over the host link (af_xdp.c:200-214 geometry)
   dma-4K      the same slots by one hipMemcpy2DAsync (PBGPU_UMEM_DMA=1)
   scatter-dense / dma-dense   the same bytes into back-to-back slots (slot = frame length)
+  scatter-<S>  power-of-two slots of S bytes between the two (a UMEM with several frames per 4 KiB)
+  dma1d-dense  the dense case as one contiguous copy (pbgpu_copy_packed: hipMemcpyAsync)
 and the build alone.  One JSON line per measurement: ms per batch, Mpps, frame GB/s."""
 import ctypes as C
 import json
@@ -42,7 +44,10 @@ def run(mode):
             ctx.build(i, r * N, N, fb)
         ctx.sync()
         out.append({"frame": flen, "what": "build only", "ms": (time.perf_counter() - t0) / REPS * 1e3})
-        for slot in (4096, flen):
+        slots = [4096, flen] + ([128, 256] if flen == 64 else [2048] if flen == 1500 else [])
+        for slot in slots:
+            if mode == "dma" and slot not in (4096, flen):
+                continue
             umem = np.zeros(N * slot + 4096, dtype=np.uint8)
             assert ctx.lib.pbgpu_host_register(ctx.h, umem.ctypes.data, umem.nbytes) == 0
             fb.to_umem(umem, slot, 0, N)  # first landing: mappings, staging
@@ -52,8 +57,15 @@ def run(mode):
             dt = (time.perf_counter() - t0) / REPS
             ok = bytes(umem[:flen]) == fb.frames()[0] if slot == 4096 else True
             ctx.lib.pbgpu_host_unregister(ctx.h, umem.ctypes.data)
-            out.append({"frame": flen, "what": f"{mode}-{'4K' if slot == 4096 else 'dense'}", "ms": dt * 1e3,
-                        "first_frame_ok": ok})
+            what = {4096: "4K", flen: "dense"}.get(slot, str(slot))
+            out.append({"frame": flen, "what": f"{mode}-{what}", "ms": dt * 1e3, "first_frame_ok": ok})
+            if slot == flen and mode == "scatter":
+                t0 = time.perf_counter()
+                for r in range(REPS):
+                    assert ctx.lib.pbgpu_copy_packed(ctx.h, fb.ptr, umem.ctypes.data, 0, N * flen) == 0
+                dt = (time.perf_counter() - t0) / REPS
+                out.append({"frame": flen, "what": "dma1d-dense", "ms": dt * 1e3,
+                            "first_frame_ok": bytes(umem[:flen]) == fb.frames()[0]})
         fb.free()
     ctx.close()
     for o in out:

@@ -20,7 +20,8 @@ class OurCmd(C.Structure):
     _fields_ = REF_FIELDS + [("gpus", C.c_int), ("gpu_first", C.c_int), ("gpu_batch", C.c_uint64),
                              ("seed_base", C.c_uint64), ("literal_payload", C.c_int), ("single_fold", C.c_int),
                              ("pcap", C.c_char_p), ("tx", C.c_char_p), ("seed_set", C.c_int),
-                             ("very_random", C.c_int), ("batch_set", C.c_int), ("umem_frames", C.c_uint32)]
+                             ("very_random", C.c_int), ("batch_set", C.c_int), ("umem_frames", C.c_uint32),
+                             ("umem_slot", C.c_uint32)]
 
 
 _libc = C.CDLL(ctypes.util.find_library("c"))

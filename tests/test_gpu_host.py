@@ -48,6 +48,40 @@ def test_cli_pcap_equals_oracle(tmp_path, batch):
     assert got == want
 
 
+@pytest.mark.parametrize("name,args,slot,threads", [
+    ("c2_udp_64", ["--protocol", "udp", "--udport", "27015", "--pmin", "22", "--pmax", "22"], 64, 1),
+    ("c2_udp_64", ["--protocol", "udp", "--udport", "27015", "--pmin", "22", "--pmax", "22", "--sharedumem"], 64, 3),
+    ("tcp60", ["--protocol", "tcp", "--tdport", "80", "--syn", "1", "--pmin", "6", "--pmax", "6"], 64, 1),
+    ("udpvar", ["--protocol", "udp", "--udport", "27015", "--pmin", "0", "--pmax", "900"], 1024, 2),
+])
+def test_cli_umemslot_pcap_equals_oracle(tmp_path, name, args, slot, threads):
+    """--umemslot S: frames land in S-byte slots (tight 64-B slots are written whole)
+    and the TX descriptors address them; the capture taken from the UMEM at the descriptors
+    equals the oracle's frames."""
+    pcap = tmp_path / "slot.pcap"
+    seed, n = 99, 6000
+    cmd = [BIN, "-z", "--interface", "pbnodev0", "--smac", pc.SMAC, "--dmac", pc.DMAC, "--dip", pc.DIP,
+           "--sip", "10.20.0.0/16"] + args + ["--maxpckts", str(n), "--delay", "0", "--gpubatch", "1000", "--seed",
+                                              str(seed), "--threads", str(threads), "--umemslot", str(slot),
+                                              "--pcap", str(pcap)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    got = read_pcap(pcap)
+    cfg = pc.c2_udp_64()  # what the -z options above give
+    cfg["payloads"] = [{"length": {"min": int(args[args.index("--pmin") + 1]),
+                                   "max": int(args[args.index("--pmax") + 1])}}]
+    if args[1] == "tcp":
+        cfg["ip"]["protocol"] = "tcp"
+        del cfg["udp"]
+        cfg["tcp"] = {"dport": 80, "syn": 1}
+    if threads == 1:
+        assert got == ob.frames(Sequence.from_config(cfg), 0, 0, n, seed)
+    else:
+        # thread t builds iterations (step * threads + t) * 1000 + j
+        assert len(got) == n and len(set(got)) == n
+        assert set(got) <= set(ob.frames(Sequence.from_config(cfg), 0, 0, 3 * n, seed))
+
+
 def test_cli_variable_tcp_time_limited(tmp_path):
     """No --smac on a device that does not exist: the source MAC stays zero with
     the reference's warnings (sequence.c:111-121)."""

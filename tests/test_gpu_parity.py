@@ -419,3 +419,42 @@ def test_umem_landing_dma_or_scatter(monkeypatch, name, dma_min):
         assert slots[n - 1, :flen].tobytes() == ob.frames(seq, 3, 9 + n - 1, 1, pc.SEED_BASE)[0]
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("name,slot,whole", [("c2_udp_64", 64, True), ("c4_tcp_syn", 64, True),
+                                             ("c5_icmp_echo", 128, True), ("c5_icmp_echo", 256, False),
+                                             ("c2_udp_1500", 2048, False), ("c2_udp_64", 128, False)])
+def test_umem_landing_tight_slots(ctx, name, slot, whole):
+    """--umemslot: slots smaller than 4 KiB.  A tight slot (no longer than the frame rounded up to
+    64 B) is written whole (the frame, then unspecified bytes: the packed stream's next ones, zeros
+    past the buffer), so back-to-back slots reach the host as contiguous writes; a wider slot gets
+    the frame's bytes only.  Every frame in its slot; nothing written outside the landed slots."""
+    seq = Sequence.from_config(pc.get(name))
+    ctx.load_sequence(9, seq, pc.SEED_BASE)
+    n = 5000
+    fb = ctx.alloc_frames(*ctx.build_size(9, n))
+    ctx.build(9, 321, n, fb)
+    ctx.sync()
+    want = ob.frames(seq, 9, 321, n, pc.SEED_BASE)
+    flen = len(want[0])
+    first, cnt, s0 = 1000, n - 1000, 7  # the landing runs to the buffer's last frame
+    umem = np.full(slot * (cnt + s0 + 3), 0xEE, dtype=np.uint8)
+    assert ctx.lib.pbgpu_host_register(ctx.h, umem.ctypes.data, umem.nbytes) == 0
+    try:
+        lens = fb.to_umem(umem, slot, first, cnt, first_slot=s0)
+    finally:
+        ctx.lib.pbgpu_host_unregister(ctx.h, umem.ctypes.data)
+    fb.free()
+    assert (lens == flen).all()
+    slots = umem.reshape(-1, slot)
+    for j in range(cnt):
+        assert slots[s0 + j, :flen].tobytes() == want[first + j], j
+    assert (slots[:s0] == 0xEE).all() and (slots[s0 + cnt:] == 0xEE).all()
+    if whole:
+        # the filler is the next frame's leading bytes (the last slot's: the buffer's tail)
+        nxt = np.frombuffer(b"".join(want[first + 1:]), dtype=np.uint8)
+        tail = slots[s0:s0 + cnt - 1, flen:]
+        assert np.array_equal(tail, np.stack([nxt[j * flen:j * flen + slot - flen] for j in range(cnt - 1)]))
+        assert (slots[s0 + cnt - 1, flen:] != 0xEE).any() or slot == flen
+    else:
+        assert (slots[s0:s0 + cnt, flen:] == 0xEE).all()

@@ -144,14 +144,18 @@ def test_af_xdp_socket_setup_fails_cleanly_without_privilege(libs):
     x = Xsk()
     umem = np.zeros(4096 * 4096 + 4096, dtype=np.uint8)
     base = (umem.ctypes.data + 4095) & ~4095
-    rc = host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096, 0, None, 0)
+    rc = host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 4096, 0, 8, -1, 0, 4096, 0, None, 0)
     # a negative errno (no AF_XDP / CAP_NET_RAW in this container), or a bound socket
     assert rc <= 0
     if rc == 0:
         host.pb_xsk_close(C.byref(x))
-    assert host.pb_xsk_open(C.byref(x), b"pbnodev0", 0, C.c_void_p(base), 4096, 4096, 8, -1, 0, 4096, 0, None, 0) == -19  # -ENODEV
+    assert host.pb_xsk_open(C.byref(x), b"pbnodev0", 0, C.c_void_p(base), 4096, 4096, 0, 8, -1, 0, 4096, 0, None,
+                            0) == -19  # -ENODEV
     # a shared-UMEM socket's slot range must lie inside the UMEM
-    assert host.pb_xsk_open(C.byref(x), b"lo", 1, C.c_void_p(base), 2048, 4096, 0, 3, 4096, 4096, 0, None, 0) == -22
+    assert host.pb_xsk_open(C.byref(x), b"lo", 1, C.c_void_p(base), 2048, 4096, 0, 0, 3, 4096, 4096, 0, None, 0) == -22
+    # slots that do not divide the registered chunk, or a UMEM that is not whole chunks
+    assert host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 4096, 96, 4096, 8, -1, 0, 4096, 0, None, 0) == -22
+    assert host.pb_xsk_open(C.byref(x), b"lo", 0, C.c_void_p(base), 64, 64, 8192, 8, -1, 0, 64, 0, None, 0) == -22
 
 
 def test_shared_umem_socket_on_the_owners_queue_needs_the_shared_ring(libs):
@@ -166,7 +170,8 @@ def test_shared_umem_socket_on_the_owners_queue_needs_the_shared_ring(libs):
     umem = np.zeros(4096 * 4096 + 4096, dtype=np.uint8)
     base = (umem.ctypes.data + 4095) & ~4095
     # a valid slot range (2048 slots from 2048 of 4096), shared fd, the owner's queue 5, no ring
-    assert host.pb_xsk_open(C.byref(x), b"lo", 5, C.c_void_p(base), 2048, 4096, 0, 3, 2048, 4096, 5, None, 1) == -22
+    assert host.pb_xsk_open(C.byref(x), b"lo", 5, C.c_void_p(base), 2048, 4096, 0, 0, 3, 2048, 4096, 5, None,
+                            1) == -22
     assert x.fd == 0 and x.umem is None  # refused before any socket was made
     r = _run(libs, _cfg(maxpckts=1000, delay=0, threads=2), shared_umem=1, queue=5, queue_set=1, tx=b"xsk")
     assert r["err"] != 0 and r["pckts"] == 0  # the socket open fails here, not a refusal up front
@@ -517,3 +522,41 @@ def test_umemframes_must_be_a_power_of_two(libs):
     host.pb_af_xdp_setup.argtypes = [C.POINTER(OurCmd), C.c_int]
     for n, ok in ((4096, True), (64, True), (1 << 20, True), (1000, False), (32, False), (1 << 21, False)):
         assert (host.pb_af_xdp_setup(C.byref(_cmd(host, umem_frames=n)), 0) == 0) == ok, n
+
+
+@pytest.mark.parametrize("slot,shared,threads,lo,hi", [(64, 0, 1, 22, 22), (64, 1, 4, 22, 22), (1024, 0, 2, 0, 900),
+                                                       (128, 1, 3, 40, 80)])
+def test_umemslot_cuts_the_umem_into_smaller_slots(libs, slot, shared, threads, lo, hi):
+    """--umemslot S: the UMEM's 4-KiB chunks cut into slots of S bytes (4096 / S frames per chunk,
+    descriptors at slot * S): exact quota, every frame once and intact in its slot, private and
+    shared UMEMs (the shared ring credits completions by slot * S)."""
+    r = _run(libs, _cfg(lo, hi, maxpckts=70000, delay=0, threads=threads), gpu_batch=20000, umem_slot=slot,
+             shared_umem=shared)
+    assert r["err"] == 0 and r["pckts"] == 70000 and r["seen"] == 70000
+    assert len(np.unique(r["k"])) == 70000 and (r["len"] != 0xFFFF).all()
+    assert r["len"].max() <= slot
+
+
+def test_umemslot_one_queue_shared_ring(libs):
+    r = _run(libs, _cfg(maxpckts=40000, delay=0, threads=3), gpu_batch=5000, umem_slot=64, shared_umem=1, queue=0,
+             queue_set=1)
+    assert r["err"] == 0 and r["pckts"] == 40000 and len(np.unique(r["k"])) == 40000
+    assert (r["len"] != 0xFFFF).all()
+
+
+def test_umemslot_refusals(libs, capfd):
+    host = libs[0]
+    host.pb_af_xdp_setup.argtypes = [C.POINTER(OurCmd), C.c_int]
+    for s, ok in ((0, True), (64, True), (4096, True), (2048, True), (32, False), (96, False), (8192, False)):
+        assert (host.pb_af_xdp_setup(C.byref(_cmd(host, umem_slot=s)), 0) == 0) == ok, s
+    # at most 2^22 slots per UMEM
+    assert host.pb_af_xdp_setup(C.byref(_cmd(host, umem_slot=64, umem_frames=1 << 16)), 0) == 0
+    assert host.pb_af_xdp_setup(C.byref(_cmd(host, umem_slot=64, umem_frames=1 << 17)), 0) == -22
+    # seq_send refuses a bad slot before the sequence takes a slot; frames longer than the slot
+    # fail their landing
+    r = _run(libs, _cfg(maxpckts=100, delay=0), umem_slot=96)
+    assert r["err"] == -22 and r["seen"] == 0
+    capfd.readouterr()
+    r = _run(libs, _cfg(0, 900, maxpckts=1000, delay=0), umem_slot=256)
+    assert r["err"] == -22 and r["pckts"] < 1000
+    assert "--umemslot" in capfd.readouterr().err
