@@ -769,10 +769,12 @@ void seq_send(const char *interface, pb_sequence_t seq, uint16_t seqc, struct cm
             return;
         }
     }
-    if (cmd.umem_slot && (cmd.umem_slot < 64 || cmd.umem_slot > PB_FRAME_SIZE || (cmd.umem_slot & (cmd.umem_slot - 1))))
+    if (cmd.umem_slot && (cmd.umem_slot < 64 || cmd.umem_slot > PB_FRAME_SIZE || (cmd.umem_slot & (cmd.umem_slot - 1)) ||
+                          (uint64_t)(cmd.umem_frames ? cmd.umem_frames : PB_NUM_FRAMES) * (PB_FRAME_SIZE / cmd.umem_slot) >
+                              (1u << 22)))
     {
-        fprintf(stderr, "[%d] --umemslot %u is not a power of two from 64 to %u.\n", seq_cnt + 1, cmd.umem_slot,
-                PB_FRAME_SIZE);
+        fprintf(stderr, "[%d] --umemslot %u is not a power of two from 64 to %u giving at most 2^22 slots.\n",
+                seq_cnt + 1, cmd.umem_slot, PB_FRAME_SIZE);
         last_error = PBGPU_EINVAL;
         return;
     }

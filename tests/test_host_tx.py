@@ -554,8 +554,9 @@ def test_umemslot_refusals(libs, capfd):
     assert host.pb_af_xdp_setup(C.byref(_cmd(host, umem_slot=64, umem_frames=1 << 17)), 0) == -22
     # seq_send refuses a bad slot before the sequence takes a slot; frames longer than the slot
     # fail their landing
-    r = _run(libs, _cfg(maxpckts=100, delay=0), umem_slot=96)
-    assert r["err"] == -22 and r["seen"] == 0
+    for kw in ({"umem_slot": 96}, {"umem_slot": 64, "umem_frames": 1 << 17}):
+        r = _run(libs, _cfg(maxpckts=100, delay=0), **kw)
+        assert r["err"] == -22 and r["seen"] == 0
     capfd.readouterr()
     r = _run(libs, _cfg(0, 900, maxpckts=1000, delay=0), umem_slot=256)
     assert r["err"] == -22 and r["pckts"] < 1000
