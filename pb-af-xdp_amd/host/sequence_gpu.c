@@ -37,6 +37,7 @@ static uint32_t env_u32(const char *name, uint32_t dflt, uint32_t lo, uint32_t h
     return v < (long)lo ? lo : (v > (long)hi ? hi : (uint32_t)v);
 }
 #define PB_BATCH_BYTES_MAX (256ull << 20) /* device bytes per frame buffer (two per worker) */
+#define PB_PACE_GRAIN_US 50.0 /* a paced submit group spans about this much of the rate (one frame at least) */
 
 static uint64_t total_pckts[PB_MAX_SEQUENCES];
 static uint64_t total_bytes[PB_MAX_SEQUENCES];
@@ -417,6 +418,20 @@ static void *gpu_worker(void *p)
         const uint64_t cap = 100000ull / ((uint64_t)seq->delay * fpi);
         batch = batch < (cap ? cap : 1) ? batch : (cap ? cap : 1);
     }
+    /* submit pacing inside a landed chunk: groups of pace_g frames, each at its due time, a group
+     * spanning ~PB_PACE_GRAIN_US of this thread's share of the rate (one frame when frames are
+     * further apart: the reference's per-packet delay, sequence.c:655-659); 0 = unpaced */
+    uint32_t pace_g = 0;
+    if (seq->pps > 0 || seq->bps > 0 || seq->delay > 0)
+    {
+        double tf = seq->delay > 0 ? (double)seq->delay * 1e-6 : 0.0; /* seconds per frame, this thread */
+        if (seq->pps > 0 && (double)w->n_shards / (double)seq->pps > tf)
+            tf = (double)w->n_shards / (double)seq->pps;
+        if (seq->bps > 0 && (double)w->n_shards * max_flen / (double)seq->bps > tf)
+            tf = (double)w->n_shards * max_flen / (double)seq->bps;
+        const double g = PB_PACE_GRAIN_US * 1e-6 / tf;
+        pace_g = g < 1.0 ? 1u : g > 65536.0 ? 65536u : (uint32_t)g;
+    }
     if ((rc = B->alloc(ctx, w->seq_idx, batch, &fr[0])) != 0 || (rc = B->alloc(ctx, w->seq_idx, batch, &fr[1])) != 0)
     {
         last_error = rc;
@@ -625,7 +640,41 @@ static void *gpu_worker(void *p)
             else
                 __atomic_add_fetch(&total_bytes[w->seq_idx], bytes, __ATOMIC_RELAXED);
             const uint32_t sent_slot = xsk.next_slot;
-            if ((rc = pb_xsk_send(&xsk, ln, n)) != 0)
+            /* the chunk in pace_g groups (all at once unpaced), each group when it is due: pps
+             * against the sequence's packets so far, bps against its bytes (this chunk's already
+             * counted: less those not yet submitted), delay per thread */
+            uint64_t left_b = bytes;
+            for (uint32_t sub = 0; sub < n;)
+            {
+                const uint32_t m = pace_g && n - sub > pace_g ? pace_g : n - sub;
+                if (pace_g && sub)
+                {
+                    double due = 0;
+                    if (seq->pps > 0)
+                        due = (double)__atomic_load_n(&total_pckts[w->seq_idx], __ATOMIC_RELAXED) / (double)seq->pps;
+                    if (seq->bps > 0)
+                    {
+                        const double db =
+                            (double)(__atomic_load_n(&total_bytes[w->seq_idx], __ATOMIC_RELAXED) - left_b) /
+                            (double)seq->bps;
+                        due = db > due ? db : due;
+                    }
+                    if (seq->delay > 0)
+                    {
+                        const double dd = (double)my_frames * (double)seq->delay * 1e-6;
+                        due = dd > due ? dd : due;
+                    }
+                    sleep_until(t0 + due);
+                }
+                if ((rc = pb_xsk_send(&xsk, ln + sub, m)) != 0)
+                    break;
+                for (uint32_t i = sub; i < sub + m; ++i)
+                    left_b -= ln[i];
+                __atomic_add_fetch(&total_pckts[w->seq_idx], m, __ATOMIC_RELAXED);
+                my_frames += m;
+                sub += m;
+            }
+            if (rc != 0)
             {
                 fprintf(stderr, "[%d][%d] ERROR - Could not send packet on AF_XDP socket (%d) :: %s.\n", seq_num, 1,
                         w->shard, strerror(-rc));
@@ -637,8 +686,6 @@ static void *gpu_worker(void *p)
                 for (uint32_t i = 0; i < n; ++i)
                     print_sent(seq_num, (uint32_t)((f0 + i) % fpi), seq, umem + (size_t)(sent_slot + i) * slot_sz,
                                ln[i]);
-            __atomic_add_fetch(&total_pckts[w->seq_idx], n, __ATOMIC_RELAXED);
-            my_frames += n;
             f0 += n;
 
             /* pacing (sequence.c:389-431, 655-659) at landing-chunk granularity: pps and

@@ -16,6 +16,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../pb-af-xdp_amd/host/sequence_gpu.h"
 #include "../pb-af-xdp_amd/host/xsk_ring.h"
@@ -297,6 +298,7 @@ typedef struct rec
 {
     uint64_t k;
     uint16_t seq_idx, i, len, thread;
+    double t; /* CLOCK_MONOTONIC seconds when the TX side took the frame */
 } rec_t;
 
 static rec_t *g_rec;
@@ -312,6 +314,9 @@ static int rec_hook(void *ctx, int thread_id, const uint8_t *frame, uint16_t len
     memcpy(&r.i, frame + 10, 2);
     memcpy(&r.len, frame + 12, 2);
     r.thread = (uint16_t)thread_id;
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    r.t = ts.tv_sec + ts.tv_nsec * 1e-9;
     if (r.len != len)
         r.len = 0xFFFF; /* the descriptor's length disagrees with the frame */
     pthread_mutex_lock(&g_rec_mu);
@@ -330,6 +335,14 @@ int stub_record(uint64_t cap)
     g_rec_n = 0;
     pb_set_tx_hook(g_rec ? rec_hook : NULL, NULL);
     return g_rec ? 0 : -12;
+}
+
+/* the recorded frames' times (up to n) */
+void stub_times(double *t, uint64_t n)
+{
+    const uint64_t m = g_rec_n < g_rec_cap ? g_rec_n : g_rec_cap;
+    for (uint64_t j = 0; j < m && j < n; ++j)
+        t[j] = g_rec[j].t;
 }
 
 /* recorded frames -> k[], i[], len[], thread[] (up to n); returns the count seen */

@@ -46,6 +46,7 @@ def libs():
     stub.stub_recorded.restype = C.c_uint64
     stub.stub_recorded.argtypes = [C.c_void_p] * 4 + [C.c_uint64]
     stub.stub_record.argtypes = [C.c_uint64]
+    stub.stub_times.argtypes = [C.c_void_p, C.c_uint64]
     yield host, stub
     stub.stub_uninstall()
     host.pb_set_tx_hook(None, None)
@@ -247,8 +248,10 @@ def _run(libs, cfg, seqc=1, cap=1 << 20, devices=None, **cmdkw):
     i, ln, th = (np.zeros(n, dtype=np.uint16) for _ in range(3))
     seen = stub.stub_recorded(k.ctypes.data, i.ctypes.data, ln.ctypes.data, th.ctypes.data, n)
     m = min(seen, n)
+    t = np.zeros(m, dtype=np.float64)
+    stub.stub_times(t.ctypes.data, m)
     return {"err": err, "pckts": p.value, "bytes": b.value, "dt": dt, "seen": seen, "k": k[:m], "i": i[:m],
-            "len": ln[:m], "thread": th[:m], "seq": s}
+            "len": ln[:m], "thread": th[:m], "t": t, "seq": s}
 
 
 def _cfg(min_len=22, max_len=22, **kw):
@@ -325,6 +328,21 @@ def test_delay_is_per_thread_and_per_packet(libs, threads, want_s):
     r = _run(libs, _cfg(maxpckts=400, delay=2000, threads=threads), gpu_batch=100000)
     assert r["pckts"] == 400
     assert want_s * 0.7 < r["dt"] < want_s * 2 + 0.4
+
+
+@pytest.mark.parametrize("kw,gap_s", [({"delay": 2000}, 0.002), ({"pps": 2000, "delay": 0}, 0.0005),
+                                      ({"bps": 128000, "delay": 0}, 0.0005)])
+def test_pacing_spreads_the_frames_of_a_batch(libs, kw, gap_s):
+    """Inside a landed batch the frames are submitted when due, one at a time at these rates
+    (the reference sleeps `delay` after every packet, sequence.c:655-659): no burst of a whole
+    batch then an idle gap, as a launch-granular pacer would send."""
+    r = _run(libs, _cfg(maxpckts=300, **kw), gpu_batch=100000)
+    assert r["err"] == 0 and r["pckts"] == 300
+    d = np.diff(r["t"])
+    assert 0.6 * gap_s < np.median(d) < 2.5 * gap_s, np.median(d)
+    # most frames leave on their own (a launch-granular pacer sends 50-200 back to back, then
+    # waits); a sender delayed by the scheduler catches up with a few at once
+    assert (d > 0.3 * gap_s).mean() > 0.7, (d > 0.3 * gap_s).mean()
 
 
 def test_default_delay_sends_one_frame_per_second_per_thread(libs):
