@@ -1,0 +1,319 @@
+// r06_vdiag.hip — where pb_vline_kernel's time goes on the round-6 kernel (tool only, never linked
+// into libpbgpu.so): a copy of the product kernel with compile-time cuts, timed beside the product
+// build and the write-roofline fills on the same buffers, to decide whether cutting its per-chunk
+// VALU work (57 instructions per 16-B chunk, 28 of them the payload bytes) can pay.
+//   DIAG 0: the product kernel (must time as pb_vline_kernel does)
+//   DIAG 1: chunks without payload bytes (a state word in every dword; lookups, masks, blend kept)
+//   DIAG 2: no chunk work: constant stores in the kernel's stream geometry (prologue kept)
+//   DIAG 4: no orbit sums in the prologue (the L4 checksum wrong; everything else kept)
+// Built by scripts/r06/build_vdiag.sh into pb-af-xdp_amd/lib/libpbprobe6v.so, driven by
+// scripts/r06/vdiag.py.
+#include "r06_probe.hip"
+
+namespace
+{
+
+template <int HL, bool L4, int DIAG>
+__global__ __launch_bounds__(PB_WG) void pr6v_vline(pb_kargs K)
+{
+    constexpr uint32_t GH = PB_VST_GHOSTS;
+    constexpr uint32_t NSP = (15 + HL + 15) / 16; // chunks a frame's header can touch
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    const uint32_t WF = K.vl_wgf;
+    const uint32_t CAP = WF + GH;
+    uint2 *const s_jt = reinterpret_cast<uint2 *>(s_dyn);             // jump[PB_JNEG - (i + HL)], i < 16
+    uint64_t *const s_st0 = reinterpret_cast<uint64_t *>(s_dyn + 32); // [0, GH]: slot starts - base0; [8, 12): S0 parts
+    uint32_t *const s_wsum = s_dyn + 56;                              // per-wave length sums
+    pb_u32x4 *const s_rec = reinterpret_cast<pb_u32x4 *>(s_dyn + 64); // {start, end, z, -} per frame slot
+    pb_u32x4 *const s_img = s_rec + CAP;                              // NSP header chunks per frame slot
+    pb_u32x4 *const s_m16 = s_img + CAP * NSP + 1;                    // after one zero chunk: byte masks
+    uint2 *const s_l48 = reinterpret_cast<uint2 *>(s_m16 + PB_VL_NMASK);
+    uint16_t *const s_map = reinterpret_cast<uint16_t *>(s_l48 + K.vl_nl48);
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t bxr = pb_xcd_region(blockIdx.x, gridDim.x); // XCD-contiguous regions
+    const uint32_t flags = K.flags;
+    const uint64_t f0 = (uint64_t)bxr * WF;
+    const uint64_t left = K.n_frames - f0;
+    const uint32_t nown = left < WF ? (uint32_t)left : WF;
+    const uint64_t fe = f0 + nown;
+
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+
+    // ---------------- prologue: one lane per frame slot ----------------
+    const int64_t fb = (int64_t)f0 - (int64_t)GH;
+    uint64_t s0_part = 0;
+    if (tid < (bxr & (PB_VL_GRP - 1u)))
+        s0_part = K.vblk_sum[(bxr & ~(PB_VL_GRP - 1u)) + tid];
+    const uint64_t s0_base = K.vblk_l2[bxr / PB_VL_GRP];
+    uint2 jtv = make_uint2(0u, 0u);
+    if (tid < 16u)
+        jtv = K.jump[PB_JNEG - (tid + HL)];
+    for (uint32_t i = tid; i < K.vl_nl48; i += PB_WG)
+        s_l48[i] = K.lcg48[i];
+    const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
+    const int64_t fj = fb + (int64_t)tid;
+    const bool valid = tid < CAP && fj >= 0 && (uint64_t)fj < fe;
+    uint32_t flen = 0, st0 = 0;
+    uint32_t d[16];
+#pragma unroll
+    for (int w = 0; w < 16; ++w)
+        d[w] = 0u;
+    uint32_t csum_v = 0; // the L4 checksum field, ORed into d[] after the scan
+    if (valid)
+    {
+        uint64_t k;
+        uint32_t pi;
+        pb_frame_index(K, (uint64_t)fj, k, pi);
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+        const uint32_t r0 = pb_rand_r(s);
+        const pb_frame_pl P = pb_payload<false>(K, s, pi);
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
+        flen = HL + P.plen;
+        st0 = P.st0;
+        if (L4)
+        {
+            // csum_tcpudp_magic / icmp_csum (sequence.c:569-594): header (+ pseudo header) words
+            // plus the payload's, from the orbit prefix sums
+            uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) + pb_halves(d[12]) +
+                          pb_halves(d[13]);
+            if (flags & PBK_PSEUDO)
+                hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
+            const uint32_t ps = (DIAG & 4) ? P.st0 : pb_orbit_sum(K, P.st0, P.plen);
+            const uint32_t c = (~pb_fold(pb_fold(hs) + ps)) & 0xFFFFu;
+            csum_v = K.csum_hi ? (c << 16) : c;
+        }
+    }
+    // frame starts: exclusive scan of the slot lengths (in-wave shuffles, wave totals via LDS)
+    uint32_t inc = flen;
+#pragma unroll
+    for (uint32_t dd = 1; dd < 64; dd <<= 1)
+    {
+        const uint32_t y = __shfl_up(inc, dd, 64);
+        inc += lane >= dd ? y : 0u;
+    }
+#pragma unroll
+    for (uint32_t dd = 32; dd > 0; dd >>= 1)
+        s0_part += __shfl_xor(s0_part, dd, 64);
+    if (lane == 63u)
+        s_wsum[wv] = inc;
+    if (lane == 0u)
+        s_st0[8 + wv] = s0_part;
+    if (tid <= GH)
+        s_st0[tid] = inc - flen;
+    if (tid < 16u)
+        s_jt[tid] = jtv;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < PB_WG / 64; ++w)
+    {
+        const uint32_t t = s_wsum[w];
+        pre += w < wv ? t : 0u;
+        tot += t;
+    }
+    uint64_t S0 = s0_base;
+#pragma unroll
+    for (uint32_t w = 0; w < PB_WG / 64; ++w)
+        S0 += s_st0[8 + w];
+    const uint64_t base0 = S0 - s_st0[GH]; // start of slot 0
+    const uint64_t start = base0 + pre + (inc - flen);
+    if (valid && tid >= GH) // own frames: the offsets' low words, the region's start
+    {
+        K.offsets32[(uint64_t)fj] = (uint32_t)start;
+        if (tid == GH)
+            K.vl_rstart[bxr] = start;
+    }
+    // region [lo, hi): lo = the 128-B line of the first own frame's start (0 for the first region),
+    // hi = the next region's lo (the launch's end for the last)
+    const bool last = fe == K.n_frames;
+    const uint64_t lo_abs = bxr ? (S0 & ~127ull) : 0ull;
+    const uint64_t hi_abs = last ? base0 + tot : ((base0 + tot) & ~127ull);
+    // ghosts: the frames before f0 that end past lo (a prefix f0 - 1, f0 - 2, ...)
+    uint32_t ng = 0;
+    if (bxr)
+        while (ng < GH && f0 > ng && base0 + s_st0[GH - ng] > lo_abs)
+            ++ng;
+    const uint32_t nfr = ng + nown; // frames with records: slot index t = tid - (GH - ng)
+    const uint64_t wbase = (base0 + s_st0[GH - ng]) & ~15ull;
+    const uint32_t lo_rel = (uint32_t)(lo_abs - wbase), hi_rel = (uint32_t)(hi_abs - wbase);
+    const int32_t tix = (int32_t)tid - (int32_t)(GH - ng);
+    if (valid && tix >= 0)
+    {
+        // the checksum only now: the orbit-table loads behind it (issued in the frame's field
+        // computation) complete under the scan and the barrier instead of before them
+#pragma unroll
+        for (uint32_t w = 0; w < 16; ++w)
+            d[w] |= w == K.csum_dw ? csum_v : 0u;
+        const uint32_t r = (uint32_t)(start - wbase);
+        const uint32_t s0 = r & 15u;
+        const uint2 jt = s_jt[s0];
+        s_rec[tix] = pb_u32x4{r >> 4, r + HL, r + flen, jt.x * st0 + jt.y};
+        // the header image shifted to byte s0 of the frame's first chunk: out dword u holds image
+        // bytes [4u - s0, 4u - s0 + 4)
+        const uint32_t q = s0 >> 2, sh = s0 & 3u;
+        uint32_t v[17];
+#pragma unroll
+        for (int u = 0; u < 17; ++u)
+        {
+            const uint32_t lo = u > 0 ? d[u - 1] : 0u, hi = u < 16 ? d[u] : 0u;
+            v[u] = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4u - sh) : hi;
+        }
+        // only the header bytes [s0, s0 + HL) of the image chunks are ever read (bytes before s0
+        // belong to the previous frame's chunk and take its payload, bytes after the header this
+        // frame's payload): NHW dwords from dword q, inside the frame's own NSP chunks
+        constexpr uint32_t NHW = (HL + 6) / 4;
+        static_assert(3 + NHW <= 4 * NSP, "image slot");
+        uint32_t *const img32 = reinterpret_cast<uint32_t *>(s_img + (uint32_t)tix * NSP) + q;
+#pragma unroll
+        for (uint32_t u = 0; u < NHW; ++u)
+            img32[u] = v[u];
+    }
+    __syncthreads();
+
+    // line map
+    const uint32_t R = hi_rel - lo_rel;
+    const uint32_t nlines = (R + 127u) >> 7;
+    if ((uint32_t)tix < nfr && tix >= 0)
+    {
+        const pb_u32x4 rc = s_rec[tix];
+        // lines whose first byte lies in this frame: the frame holding it, and where (if at all)
+        // the next frame starts in the line
+        const uint32_t st = rc[1] - HL;
+        const uint32_t a = st > lo_rel ? st - lo_rel : 0u, b = rc[2] > lo_rel ? rc[2] - lo_rel : 0u;
+        const uint32_t la = (a + 127u) >> 7, lb = min((b + 127u) >> 7, nlines);
+        // the next two frames' starts in the line as 16-B chunk positions c = ceil(o / 16) (1..8,
+        // 8: none), kept as 8 - c in bits 0-2 and 4-6: chunk k of the line lies in frame
+        // tix + (k >= c1) + (k >= c2), and k >= c <=> k + (8 - c) carries into bit 3 / 7
+        const uint32_t b2 = (uint32_t)tix + 1u < nfr ? s_rec[tix + 1][2] - lo_rel : 0xFFFFFFFFu;
+        // only the frame's last line can hold the next frame starts (o1, o2 >= 128 before it)
+        for (uint32_t L = la; L + 1u < lb; ++L)
+            s_map[L] = (uint16_t)((uint32_t)tix << 8);
+        if (la < lb)
+        {
+            const uint32_t L = lb - 1u;
+            const uint32_t o1 = b - (L << 7), o2 = b2 - (L << 7);
+            const uint32_t c1 = o1 < 128u ? (o1 + 15u) >> 4 : 8u, c2 = o2 < 128u ? (o2 + 15u) >> 4 : 8u;
+            s_map[L] = (uint16_t)(((uint32_t)tix << 8) | (8u - c1) | ((8u - c2) << 4));
+        }
+    }
+    // chunk byte masks, indexed by plo + phi: a chunk holds a payload start (plo > 0, phi = 16) or
+    // a payload end (plo = 0, phi < 16) or neither (payloads of >= 32 B), so s_m16[j] keeps bytes
+    // < j for j <= 16 and bytes >= j - 16 above
+    if (tid <= 32u)
+    {
+        const int lo = tid > 16u ? (int)tid - 16 : 0, hi = tid > 16u ? 16 : (int)tid;
+        s_m16[tid] = pb_u32x4{pb_range_mask(lo, hi), pb_range_mask(lo - 4, hi - 4), pb_range_mask(lo - 8, hi - 8),
+                              pb_range_mask(lo - 12, hi - 12)};
+    }
+    if (tid == 64u) // the header chunk after the last record's: no frame starts there
+        s_img[nfr * NSP] = pb_u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+
+    // ---------------- stream: the region in 16-KiB steps, no barriers ----------------
+    // Chunk ci (16-B units from wbase) of line l: frame f holds its first byte, and its bytes are
+    // f's payload bytes in [plo, phi) (one generated chunk, masked) and header bytes elsewhere:
+    // f's own (chunk m < NSP of f: the shifted image, bytes < plo) or the next frame's, which
+    // starts inside the chunk when phi < 16 (then m >= NSP, and image slot f * NSP + NSP is the
+    // next frame's first chunk, bytes >= phi; for a chunk with neither both masks are empty).
+    // One straight-line path per chunk, and every 128-B line leaves in one store instruction.
+    uint8_t *const gout = K.out + wbase + lo_rel;
+    const uint32_t nsteps = (R + PB_VL_STEP - 1u) / PB_VL_STEP;
+    const uint32_t k = lane & 7u, kk = k | (k << 4), ck = (lo_rel >> 4) + k;
+    const uint32_t lmax = nlines ? nlines - 1u : 0u;
+    // chunk i of step s; clamp: lines past the region's end are computed on its last line
+    auto chunk = [&](uint32_t s, uint32_t i, bool clamp) -> pb_u32x4 {
+        if (DIAG & 2) // no chunk work: the stream's stores alone
+            return pb_u32x4{s, i, lane, 0x5EEDu};
+        uint32_t l = s * (PB_VL_STEP / 128u) + (wv << 5) + (i << 3) + (lane >> 3);
+        if (clamp)
+            l = min(l, lmax);
+        const uint32_t ci = (l << 3) + ck;
+        const uint32_t t = (uint32_t)s_map[l] + kk;
+        const uint32_t f = (t >> 8) + __popc(t & 0x88u);
+        const pb_u32x4 rc = s_rec[f];
+        const uint32_t m = ci - rc[0]; // chunk index within frame f
+        const uint2 L = s_l48[m];
+        const uint32_t x = __umul24(rc[3], L.x) + L.y;
+        const int32_t pb = (int32_t)(ci << 4);
+        const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
+        const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
+        const pb_u32x4 h = s_img[f * NSP + min(m, NSP)];
+        uint32_t o0, o1, o2, o3;
+        if (DIAG & 1) // no payload bytes: one state word in every dword
+            o0 = o1 = o2 = o3 = x;
+        else
+            pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+        const pb_u32x4 mm = s_m16[plo + phi]; // payload bytes [plo, phi)
+        const uint32_t M0 = mm[0], M1 = mm[1], M2 = mm[2], M3 = mm[3];
+        return pb_u32x4{(o0 & M0) | (h[0] & ~M0), (o1 & M1) | (h[1] & ~M1), (o2 & M2) | (h[2] & ~M2),
+                        (o3 & M3) | (h[3] & ~M3)};
+    };
+    // steps that lie wholly inside the region: no clamp, no store guard (their four chunks' LCG
+    // chains interleave instead of each running inside its own store branch)
+    const uint32_t nfull = min(nsteps, R / PB_VL_STEP);
+    for (uint32_t s = 0; s < nfull; ++s)
+    {
+        pb_u32x4 v[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            v[i] = chunk(s, i, false);
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            pb_st16_nt(gout + s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4), v[i]);
+    }
+    for (uint32_t s = nfull; s < nsteps; ++s)
+    {
+        // four independent chunks per lane, computed before any is stored
+        pb_u32x4 v[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            v[i] = chunk(s, i, true);
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+        {
+            const uint32_t c0 = s * PB_VL_STEP + (wv << 12) + (i << 10) + (lane << 4);
+            if (c0 < R)
+                pb_st16_nt(gout + c0, v[i]);
+        }
+    }
+    if (tid == 0) // the workgroup stores exactly [lo, hi) (the launch's last chunk zero-padded)
+        pb_count(K, bxr, nown, hi_abs - lo_abs);
+}
+
+
+} // namespace
+
+extern "C" {
+
+// the product build's kargs for `seq` into `out`, then the DIAG copy timed (reps launches)
+int pr6v_run(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, int diag, int reps,
+             double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr6_kargs(ctx, seq, first, n, out, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    if (!K.vl || K.hl != 42 || !(K.flags & PBK_L4_CSUM))
+        return PBGPU_EINVAL;
+    const uint32_t grid = (uint32_t)((K.n_frames + K.vl_wgf - 1) / K.vl_wgf);
+    const size_t lds = PB_VL_LDS(K.vl_wgf, 4, K.vl_nl48, K.vl_nlines) + K.lds_pad;
+    hipStream_t st = ctx->stream;
+    auto launch = [&]() -> hipError_t {
+        switch (diag)
+        {
+        case 0: hipLaunchKernelGGL((pr6v_vline<42, true, 0>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 1: hipLaunchKernelGGL((pr6v_vline<42, true, 1>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 2: hipLaunchKernelGGL((pr6v_vline<42, true, 2>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 4: hipLaunchKernelGGL((pr6v_vline<42, true, 4>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 5: hipLaunchKernelGGL((pr6v_vline<42, true, 5>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 6: hipLaunchKernelGGL((pr6v_vline<42, true, 6>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    };
+    return pr6_time(ctx, reps, ms, launch);
+}
+
+} // extern "C"
