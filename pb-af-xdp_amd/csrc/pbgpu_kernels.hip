@@ -188,6 +188,31 @@ __device__ __forceinline__ uint32_t pb_mad24v(uint32_t x, uint32_t a, uint32_t c
     return r;
 }
 
+// Opaque one-instruction forms for pb_vline_kernel's chunk addressing: the compiler schedules them
+// but cannot strength-reduce them into longer loop-carried chains (it turned `ci - rc0` into three
+// instructions per chunk).  a - b:
+__device__ __forceinline__ uint32_t pb_subv(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_sub_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// c - 256 a, a < 2^23 (c any 32-bit value; the multiplier in an SGPR: VOP3 takes no literal here)
+__device__ __forceinline__ int32_t pb_msub256(uint32_t a, uint32_t c)
+{
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(-256), "v"(c));
+    return r;
+}
+// (a << SH) + b
+template <int SH>
+__device__ __forceinline__ uint32_t pb_lshl_add(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(SH), "v"(b));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t pb_vgpr(uint32_t s)
 {
     uint32_t v;
@@ -2677,7 +2702,8 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         const uint32_t r = (uint32_t)(start - wbase);
         const uint32_t s0 = r & 15u;
         const uint2 jt = s_jt[s0];
-        s_rec[tix] = pb_u32x4{r >> 4, r + HL, r + flen, jt.x * st0 + jt.y};
+        // payload start and end in 1/16 B (the chunk masks are then indexed without shifts)
+        s_rec[tix] = pb_u32x4{r >> 4, (r + HL) << 4, (r + flen) << 4, jt.x * st0 + jt.y};
         // the header image shifted to byte s0 of the frame's first chunk: out dword u holds image
         // bytes [4u - s0, 4u - s0 + 4)
         const uint32_t q = s0 >> 2, sh = s0 & 3u;
@@ -2708,13 +2734,13 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         const pb_u32x4 rc = s_rec[tix];
         // lines whose first byte lies in this frame: the frame holding it, and where (if at all)
         // the next frame starts in the line
-        const uint32_t st = rc[1] - HL;
-        const uint32_t a = st > lo_rel ? st - lo_rel : 0u, b = rc[2] > lo_rel ? rc[2] - lo_rel : 0u;
+        const uint32_t st = (rc[1] >> 4) - HL, end = rc[2] >> 4;
+        const uint32_t a = st > lo_rel ? st - lo_rel : 0u, b = end > lo_rel ? end - lo_rel : 0u;
         const uint32_t la = (a + 127u) >> 7, lb = min((b + 127u) >> 7, nlines);
         // the next two frames' starts in the line as 16-B chunk positions c = ceil(o / 16) (1..8,
         // 8: none), kept as 8 - c in bits 0-2 and 4-6: chunk k of the line lies in frame
         // tix + (k >= c1) + (k >= c2), and k >= c <=> k + (8 - c) carries into bit 3 / 7
-        const uint32_t b2 = (uint32_t)tix + 1u < nfr ? s_rec[tix + 1][2] - lo_rel : 0xFFFFFFFFu;
+        const uint32_t b2 = (uint32_t)tix + 1u < nfr ? (s_rec[tix + 1][2] >> 4) - lo_rel : 0xFFFFFFFFu;
         // only the frame's last line can hold the next frame starts (o1, o2 >= 128 before it)
         for (uint32_t L = la; L + 1u < lb; ++L)
             s_map[L] = (uint16_t)((uint32_t)tix << 8);
@@ -2759,16 +2785,16 @@ __global__ __launch_bounds__(PB_WG) void pb_vline_kernel(pb_kargs K)
         const uint32_t t = (uint32_t)s_map[l] + kk;
         const uint32_t f = (t >> 8) + __popc(t & 0x88u);
         const pb_u32x4 rc = s_rec[f];
-        const uint32_t m = ci - rc[0]; // chunk index within frame f
+        const uint32_t m = pb_subv(ci, rc[0]); // chunk index within frame f
         const uint2 L = s_l48[m];
         const uint32_t x = __umul24(rc[3], L.x) + L.y;
-        const int32_t pb = (int32_t)(ci << 4);
-        const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
-        const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
-        const pb_u32x4 h = s_img[f * NSP + min(m, NSP)];
+        // payload bytes [plo, phi) of the chunk, in 1/16 B: 16 plo + 16 phi is s_m16's byte offset
+        const uint32_t plo16 = (uint32_t)min(max(pb_msub256(ci, rc[1]), 0), 256);
+        const uint32_t phi16 = (uint32_t)min(max(pb_msub256(ci, rc[2]), 0), 256);
+        const pb_u32x4 h = s_img[NSP == 4 ? pb_lshl_add<2>(f, min(m, NSP)) : f * NSP + min(m, NSP)];
         uint32_t o0, o1, o2, o3;
         pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
-        const pb_u32x4 mm = s_m16[plo + phi]; // payload bytes [plo, phi)
+        const pb_u32x4 mm = *reinterpret_cast<const pb_u32x4 *>(reinterpret_cast<const uint8_t *>(s_m16) + plo16 + phi16);
         const uint32_t M0 = mm[0], M1 = mm[1], M2 = mm[2], M3 = mm[3];
         return pb_u32x4{(o0 & M0) | (h[0] & ~M0), (o1 & M1) | (h[1] & ~M1), (o2 & M2) | (h[2] & ~M2),
                         (o3 & M3) | (h[3] & ~M3)};

@@ -13,6 +13,37 @@
 namespace
 {
 
+// opaque VALU forms (the compiler may schedule them but not rewrite them into longer chains)
+__device__ __forceinline__ uint32_t pr6v_sub(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_sub_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// c - 16 a (a < 2^23, c < 2^23 signed)
+__device__ __forceinline__ int32_t pr6v_msub16(uint32_t a, uint32_t c)
+{
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, -16, %2" : "=v"(r) : "v"(a), "v"(c));
+    return r;
+}
+
+// c - 256 a with the multiplier in an SGPR (VOP3 takes no literal on gfx950)
+__device__ __forceinline__ int32_t pr6v_msub256(uint32_t a, uint32_t c)
+{
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(-256), "v"(c));
+    return r;
+}
+// (a << sh) + b, kept as one v_lshl_add_u32
+template <int SH>
+__device__ __forceinline__ uint32_t pr6v_lshl_add(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(SH), "v"(b));
+    return r;
+}
+
 template <int HL, bool L4, int DIAG>
 __global__ __launch_bounds__(PB_WG) void pr6v_vline(pb_kargs K)
 {
@@ -148,7 +179,10 @@ __global__ __launch_bounds__(PB_WG) void pr6v_vline(pb_kargs K)
         const uint32_t r = (uint32_t)(start - wbase);
         const uint32_t s0 = r & 15u;
         const uint2 jt = s_jt[s0];
-        s_rec[tix] = pb_u32x4{r >> 4, r + HL, r + flen, jt.x * st0 + jt.y};
+        if (DIAG & 32) // payload bounds in 1/16 B: the chunk masks index without shifts
+            s_rec[tix] = pb_u32x4{r >> 4, (r + HL) << 4, (r + flen) << 4, jt.x * st0 + jt.y};
+        else
+            s_rec[tix] = pb_u32x4{r >> 4, r + HL, r + flen, jt.x * st0 + jt.y};
         // the header image shifted to byte s0 of the frame's first chunk: out dword u holds image
         // bytes [4u - s0, 4u - s0 + 4)
         const uint32_t q = s0 >> 2, sh = s0 & 3u;
@@ -176,7 +210,9 @@ __global__ __launch_bounds__(PB_WG) void pr6v_vline(pb_kargs K)
     const uint32_t nlines = (R + 127u) >> 7;
     if ((uint32_t)tix < nfr && tix >= 0)
     {
-        const pb_u32x4 rc = s_rec[tix];
+        pb_u32x4 rc = s_rec[tix];
+        if (DIAG & 32)
+            rc[1] >>= 4, rc[2] >>= 4;
         // lines whose first byte lies in this frame: the frame holding it, and where (if at all)
         // the next frame starts in the line
         const uint32_t st = rc[1] - HL;
@@ -185,7 +221,7 @@ __global__ __launch_bounds__(PB_WG) void pr6v_vline(pb_kargs K)
         // the next two frames' starts in the line as 16-B chunk positions c = ceil(o / 16) (1..8,
         // 8: none), kept as 8 - c in bits 0-2 and 4-6: chunk k of the line lies in frame
         // tix + (k >= c1) + (k >= c2), and k >= c <=> k + (8 - c) carries into bit 3 / 7
-        const uint32_t b2 = (uint32_t)tix + 1u < nfr ? s_rec[tix + 1][2] - lo_rel : 0xFFFFFFFFu;
+        const uint32_t b2 = (uint32_t)tix + 1u < nfr ? (s_rec[tix + 1][2] >> ((DIAG & 32) ? 4 : 0)) - lo_rel : 0xFFFFFFFFu;
         // only the frame's last line can hold the next frame starts (o1, o2 >= 128 before it)
         for (uint32_t L = la; L + 1u < lb; ++L)
             s_map[L] = (uint16_t)((uint32_t)tix << 8);
@@ -232,19 +268,33 @@ __global__ __launch_bounds__(PB_WG) void pr6v_vline(pb_kargs K)
         const uint32_t t = (uint32_t)s_map[l] + kk;
         const uint32_t f = (t >> 8) + __popc(t & 0x88u);
         const pb_u32x4 rc = s_rec[f];
-        const uint32_t m = ci - rc[0]; // chunk index within frame f
+        const uint32_t m = (DIAG & 16) ? pr6v_sub(ci, rc[0]) : ci - rc[0]; // chunk index within frame f
         const uint2 L = s_l48[m];
         const uint32_t x = __umul24(rc[3], L.x) + L.y;
         const int32_t pb = (int32_t)(ci << 4);
-        const uint32_t plo = (uint32_t)min(max((int32_t)rc[1] - pb, 0), 16);
-        const uint32_t phi = (uint32_t)min(max((int32_t)rc[2] - pb, 0), 16);
-        const pb_u32x4 h = s_img[f * NSP + min(m, NSP)];
+        pb_u32x4 h, mm;
+        if (DIAG & 32)
+        {
+            // plo, phi in 1/16 B: s_m16 is indexed by (plo + phi) 16-B rows, i.e. bytes
+            const uint32_t plo16 = (uint32_t)min(max(pr6v_msub256(ci, rc[1]), 0), 256);
+            const uint32_t phi16 = (uint32_t)min(max(pr6v_msub256(ci, rc[2]), 0), 256);
+            mm = *reinterpret_cast<const pb_u32x4 *>(reinterpret_cast<const uint8_t *>(s_m16) + plo16 + phi16);
+            h = s_img[pr6v_lshl_add<2>(f, min(m, NSP))];
+        }
+        else
+        {
+            const int32_t p1 = (DIAG & 16) ? pr6v_msub16(ci, rc[1]) : (int32_t)rc[1] - pb;
+            const int32_t p2 = (DIAG & 16) ? pr6v_msub16(ci, rc[2]) : (int32_t)rc[2] - pb;
+            const uint32_t plo = (uint32_t)min(max(p1, 0), 16);
+            const uint32_t phi = (uint32_t)min(max(p2, 0), 16);
+            h = s_img[f * NSP + min(m, NSP)];
+            mm = s_m16[plo + phi]; // payload bytes [plo, phi)
+        }
         uint32_t o0, o1, o2, o3;
         if (DIAG & 1) // no payload bytes: one state word in every dword
             o0 = o1 = o2 = o3 = x;
         else
             pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
-        const pb_u32x4 mm = s_m16[plo + phi]; // payload bytes [plo, phi)
         const uint32_t M0 = mm[0], M1 = mm[1], M2 = mm[2], M3 = mm[3];
         return pb_u32x4{(o0 & M0) | (h[0] & ~M0), (o1 & M1) | (h[1] & ~M1), (o2 & M2) | (h[2] & ~M2),
                         (o3 & M3) | (h[3] & ~M3)};
@@ -309,6 +359,10 @@ int pr6v_run(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_fra
         case 4: hipLaunchKernelGGL((pr6v_vline<42, true, 4>), dim3(grid), dim3(PB_WG), lds, st, K); break;
         case 5: hipLaunchKernelGGL((pr6v_vline<42, true, 5>), dim3(grid), dim3(PB_WG), lds, st, K); break;
         case 6: hipLaunchKernelGGL((pr6v_vline<42, true, 6>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 16: hipLaunchKernelGGL((pr6v_vline<42, true, 16>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 17: hipLaunchKernelGGL((pr6v_vline<42, true, 17>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 48: hipLaunchKernelGGL((pr6v_vline<42, true, 48>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 49: hipLaunchKernelGGL((pr6v_vline<42, true, 49>), dim3(grid), dim3(PB_WG), lds, st, K); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

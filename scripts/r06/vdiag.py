@@ -1,5 +1,5 @@
 """pb_vline_kernel decomposition (libpbprobe6v.so from probes/r06_vdiag.hip; tool only).
-python3 scripts/r06/vdiag.py [reps] [nbuf]
+python3 scripts/r06/vdiag.py [reps] [nbuf] [diag,diag,...]
 configs[2] (2^25 frames) into nbuf buffers alive at once; per buffer, round after round: the product
 build (pr6_build: pb_vline_kernel), its copy with compile-time cuts (DIAG 0 uncut, 1 no payload
 bytes, 2 no chunk work, 4 no orbit sums, 5 = 1 + 4, 6 = 2 + 4) and the write-roofline fills over
@@ -32,8 +32,27 @@ def ok(rc, what):
         raise SystemExit(f"{what}: rc {rc}")
 
 
-n = 1 << 25
+DIAGS = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 1, 2, 4, 5, 6]
 ctx.load_sequence(0, Sequence.from_config(pc.get("c3_udp_var")), pc.SEED_BASE)
+# the cuts that keep the bytes (0, 16, 32, 48) must build exactly the product's frames: 2^20 frames
+m = 1 << 20
+a = ctx.alloc_frames(*ctx.build_size(0, m))
+b = ctx.alloc_frames(*ctx.build_size(0, m))
+ctx.build(0, 12345, m, a)
+ctx.sync()
+want, want_off = a.packed().copy(), a.offsets().copy()
+for dg in DIAGS:
+    if dg & 7:
+        continue
+    ok(L.pr6v_run(ctx.h, 0, 12345, m, b.ptr, dg, 1, C.byref(D())), f"check {dg}")
+    ctx.sync()
+    same = bool((b.packed() == want).all()) and bool((b.offsets() == want_off).all())
+    print(json.dumps({"check": dg, "frames": m, "bit_exact": same}), flush=True)
+    if not same:
+        raise SystemExit(f"diag {dg} differs from the product build")
+a.free()
+b.free()
+n = 1 << 25
 bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(NBUF)]
 for fb in bufs:
     ctx.build(0, 0, n, fb)
@@ -48,7 +67,7 @@ for r in range(REPS):
     for b, fb in enumerate(bufs):
         ok(L.pr6_build(ctx.h, 0, 0, n, fb.ptr, 10, C.byref(ms)), "build")
         res.setdefault((b, "product"), []).append(ms.value)
-        for dg in (0, 1, 2, 4, 5, 6):
+        for dg in DIAGS:
             ok(L.pr6v_run(ctx.h, 0, 0, n, fb.ptr, dg, 10, C.byref(ms)), f"diag {dg}")
             res.setdefault((b, f"diag{dg}"), []).append(ms.value)
         for name, mode in (("fill 4KiB/wg", 2), ("fill 4KiB/wg 4/CU", 5), ("fill 208KiB regions", 12)):
