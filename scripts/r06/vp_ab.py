@@ -1,6 +1,7 @@
 """configs[2] kernels side by side in one process on the same buffers (tool only):
 python3 scripts/r06/vp_ab.py [reps] [nbuf] [variants...]
-variants: PBGPU_KERNEL values to load (default: "" = the library default, and "vline"); each is
+variants: PBGPU_KERNEL values, or VAR=val[,VAR2=val2] load-time settings, to load (default: "" = the
+library default, and "vpage"); each is
 loaded into its own slot, then every buffer is built by every variant, reps rounds, 10 launches per
 timing (TIMING_LAUNCH medians).  One JSON line per (buffer, variant)."""
 import json
@@ -21,15 +22,18 @@ n = 1 << 25
 ctx = GpuContext(0)
 seq = Sequence.from_config(pc.get("c3_udp_var"))
 names = {}
+ENV_KEYS = {"PBGPU_KERNEL"}
 for i, v in enumerate(VARS):
     # (the round-6 forms vpage:512 and vpage:pool selected kernels since removed)
-    if v:
-        os.environ["PBGPU_KERNEL"] = v
-    else:
-        os.environ.pop("PBGPU_KERNEL", None)
+    env = dict(e.split("=", 1) for e in v.split(",")) if "=" in v else {"PBGPU_KERNEL": v} if v else {}
+    for key in set(ENV_KEYS) | set(env):
+        os.environ.pop(key, None)
+    os.environ.update(env)
+    ENV_KEYS.update(env)
     ctx.load_sequence(i, seq, pc.SEED_BASE)
     names[i] = ctx.kernel_name(i)
-os.environ.pop("PBGPU_KERNEL", None)
+for key in ENV_KEYS:
+    os.environ.pop(key, None)
 bufs = [ctx.alloc_frames(*ctx.build_size(0, n)) for _ in range(NBUF)]
 ctx.set_timing(ctx.TIMING_LAUNCH)
 t0 = time.perf_counter()
