@@ -332,6 +332,206 @@ __global__ __launch_bounds__(PB_WG) void pr6v_vline(pb_kargs K)
 }
 
 
+template <int G, bool L4, int DIAG>
+__global__ __launch_bounds__(PB_WG) void pr6v_fstage(pb_kargs K)
+{
+    constexpr uint32_t NGW = PB_WG / G; // frames per window
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    const uint32_t SB = K.fst_sb, NB = K.fst_nbuf, WF = K.fst_wgf;
+    uint8_t *const stage = reinterpret_cast<uint8_t *>(s_dyn);
+    uint32_t *const s_img = s_dyn + ((NB * SB) >> 2); // header image, 16 dwords per frame
+    uint32_t *const s_z = s_img + WF * 16;             // LCG state at the frame's first 16-B chunk
+    uint32_t *const s_a0 = s_z + WF;                   // lane 0's initial checksum accumulator
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t flags = K.flags;
+    const uint32_t flen = K.fixed_len, hl = K.hl;
+    const uint64_t f0 = (uint64_t)pb_xcd_region(blockIdx.x, gridDim.x) * WF;
+    const uint64_t left = K.n_frames - f0;
+    const uint32_t nfr = left < WF ? (uint32_t)left : WF;
+    const uint64_t W0 = f0 * flen; // 16-B aligned
+
+    // lane constants: group grp builds frame w * NGW + grp of every window w
+    const uint32_t grp = tid / G, lg = tid % G;
+    const uint32_t r = grp * flen; // frame start, relative to its window
+    const uint32_t s0 = r & 15u;
+    const uint32_t ma = (s0 + hl) >> 4;           // first chunk holding payload
+    const uint32_t nch = (s0 + flen + 15u) >> 4;  // chunks the frame touches
+    const uint32_t e4 = ((s0 + flen) & 15u) >> 2; // dwords of the frame in its last chunk (0: all 4)
+    const uint32_t mlast = nch - 1u - lg;         // this lane's last chunk
+    const uint32_t cnt = mlast >= ma && mlast < nch ? (mlast - ma) / G + 1u : 0u;
+    const uint32_t mfirst = mlast - (cnt ? cnt - 1u : 0u) * G;
+    const uint2 Mm = K.lcg48[cnt ? mfirst : 0u];
+    const uint2 MG = K.lcg48[G];
+    const uint32_t mgy = pb_vgpr(MG.y);
+    const bool tail = lg == 0 && e4 != 0; // lane 0's final chunk is cut at dword e4
+
+    // ---------------- A: one lane per frame ----------------
+    const uint2 rg1 = (flags & PBK_RND_SADDR) ? K.ranges[0] : make_uint2(0u, 0u);
+    if (tid < nfr)
+    {
+        const uint64_t f = f0 + tid;
+        const uint32_t hs0 = (((tid % NGW) * flen) & 15u) + hl;
+        const uint2 jt = K.jump[PB_JNEG - hs0];
+        const int j0 = (int)(16u * (hs0 >> 4)) - (int)hs0; // (-16, 0]: header bytes in chunk ma
+        const uint2 ja = K.jump[PB_JNEG + j0];
+        uint64_t k;
+        uint32_t pi;
+        pb_frame_index(K, f, k, pi);
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+        const uint32_t r0 = pb_rand_r(s);
+        const pb_frame_pl P = pb_payload<false>(K, s, pi);
+        uint32_t d[16];
+        const uint32_t l4tot = pb_header(K, r0, P.plen, d, K.rng.d == 1 ? rg1 : pb_range(K, r0));
+        pb_u32x4 *row = reinterpret_cast<pb_u32x4 *>(s_img + tid * 16);
+        row[0] = pb_u32x4{d[0], d[1], d[2], d[3]};
+        row[1] = pb_u32x4{d[4], d[5], d[6], d[7]};
+        row[2] = pb_u32x4{d[8], d[9], d[10], d[11]};
+        row[3] = pb_u32x4{d[12], d[13], d[14], d[15]};
+        s_z[tid] = jt.x * P.st0 + jt.y;
+        if (L4)
+        {
+            uint32_t hs = (d[8] >> 16) + pb_halves(d[9]) + pb_halves(d[10]) + pb_halves(d[11]) +
+                          pb_halves(d[12]) + pb_halves(d[13]);
+            if (flags & PBK_PSEUDO)
+                hs += (d[6] >> 16) + pb_halves(d[7]) + (d[8] & 0xFFFFu) + ((K.proto + l4tot) << 8);
+            // the generated header bytes of chunk ma, in output alignment (frames start on even bytes)
+            uint32_t gs = 0;
+            uint32_t x = ja.x * P.st0 + ja.y;
+            for (int p = 0; p < -j0; ++p)
+            {
+                gs += ((x >> 16) & 0xFFu) << (8 * (p & 1));
+                x = pb_step3(x, PB_A3, PB_C3);
+            }
+            // one's-complement arithmetic is mod 0xFFFF: add a multiple of it to stay >= 0
+            s_a0[tid] = (DIAG & 16) ? hs : hs + 16u * 0xFFFFu - gs;
+        }
+    }
+    else if ((DIAG & 16) && L4 && tid >= 64u && tid - 64u < nfr)
+    {
+        // wave 1: the payload's word sum of frame tid - 64 from the orbit prefix sums (pb_orbit_sum),
+        // beside wave 0's headers: the payload pass then sums nothing
+        uint64_t k;
+        uint32_t pi;
+        pb_frame_index(K, f0 + (tid - 64u), k, pi);
+        const uint32_t s = pb_seed(K.seed_base, K.seq, K.first_iter + k);
+        const pb_frame_pl P = pb_payload<false>(K, s, pi);
+        s_a0[WF + tid - 64u] = pb_orbit_sum(K, P.st0, P.plen);
+    }
+    __syncthreads();
+
+    const uint32_t nwin = (nfr + NGW - 1) / NGW;
+    const uint32_t hw = hl >> 2; // header dwords written whole; hl % 4 == 2: one more half dword
+    uint32_t sb = 0;
+    for (uint32_t w = 0; w < nwin; ++w)
+    {
+        uint8_t *const stg = stage + sb;
+        const uint32_t nfw = min(NGW, nfr - w * NGW);
+        const uint32_t fr = w * NGW + grp;
+        const bool live = grp < nfw;
+        // ---------------- B: payload chunks, then the group's header ----------------
+        uint32_t acc = 0;
+        if (live && cnt && !(DIAG & 2))
+        {
+            if (L4 && lg == 0 && !(DIAG & 16))
+                acc = s_a0[fr];
+            uint32_t x = __umul24(s_z[fr], Mm.x) + Mm.y;
+            pb_u32x4 *p = reinterpret_cast<pb_u32x4 *>(stg) + (r >> 4) + mfirst;
+            uint32_t o0, o1, o2, o3;
+            for (uint32_t i = 1; i < cnt; ++i)
+            {
+                if (DIAG & 1)
+                    o0 = o1 = o2 = o3 = x;
+                else
+                    pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+                if (L4 && !(DIAG & 24))
+                    acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
+                *p = pb_u32x4{o0, o1, o2, o3};
+                p += G;
+                x = pb_mad24(x, MG.x, mgy);
+            }
+            // the lane's final chunk
+            if (DIAG & 1)
+                o0 = o1 = o2 = o3 = x;
+            else
+                pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+            if (tail)
+            {
+                uint32_t *q = reinterpret_cast<uint32_t *>(p);
+                o1 = e4 > 1u ? o1 : 0u;
+                o2 = e4 > 2u ? o2 : 0u;
+                o3 = 0u;
+                q[0] = o0;
+                if (e4 > 1u)
+                    q[1] = o1;
+                if (e4 > 2u)
+                    q[2] = o2;
+            }
+            else
+                *p = pb_u32x4{o0, o1, o2, o3};
+            if (L4 && !(DIAG & 16))
+                acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
+        }
+        if (L4 && !(DIAG & 16))
+            acc = pb_group_sum<G>(acc);
+        if (live && lg <= hw)
+        {
+            uint32_t v = s_img[fr * 16 + lg];
+            if (L4)
+            {
+                const uint32_t c = (DIAG & 16) ? (~pb_fold(pb_fold(s_a0[fr]) + s_a0[WF + fr])) & 0xFFFFu
+                                               : (~pb_fold(acc)) & 0xFFFFu;
+                if (lg == K.csum_dw)
+                    v |= K.csum_hi ? (c << 16) : c;
+            }
+            uint32_t *hp = reinterpret_cast<uint32_t *>(stg + r) + lg;
+            if (lg < hw)
+                *hp = v;
+            else if (hl & 2u)
+                *reinterpret_cast<uint16_t *>(hp) = (uint16_t)v;
+        }
+        __syncthreads();
+
+        // ---------------- S: the window to HBM, contiguous 16-B stores ----------------
+        // window bytes [0, R1); a last chunk that is not whole (the launch's last,
+        // short window) is stored dword by dword.  Lane t stores the window's chunks
+        // whose absolute 16-B index is t mod 256, so each wave's store instruction
+        // covers one 1 KiB-aligned block and each step of the workgroup one 4 KiB
+        // page (wave stores straddling 1 KiB boundaries cost ~10% of the write
+        // rate: profiles/r01/wbench, shifted pages)
+        const uint32_t R1 = nfw * flen;
+        const uint32_t c1 = R1 >> 4;
+        const uint64_t gb = W0 + (uint64_t)w * NGW * flen;
+        uint8_t *const gout = K.out + gb;
+        const pb_u32x4 *const st16 = reinterpret_cast<const pb_u32x4 *>(stg);
+        uint32_t c = (tid - (uint32_t)(gb >> 4)) & (PB_WG - 1u);
+        for (; c + 3 * PB_WG < c1; c += 4 * PB_WG)
+        {
+            const pb_u32x4 v0 = st16[c], v1 = st16[c + PB_WG], v2 = st16[c + 2 * PB_WG], v3 = st16[c + 3 * PB_WG];
+            pb_st16(gout + 16 * c, v0);
+            pb_st16(gout + 16 * (c + PB_WG), v1);
+            pb_st16(gout + 16 * (c + 2 * PB_WG), v2);
+            pb_st16(gout + 16 * (c + 3 * PB_WG), v3);
+        }
+        for (; c < c1; c += PB_WG)
+            pb_st16(gout + 16 * c, st16[c]);
+        if (tid == PB_WG - 1 && (R1 & 15u))
+        {
+            const uint32_t *sw = reinterpret_cast<const uint32_t *>(stg) + 4 * c1;
+            uint32_t *gw = reinterpret_cast<uint32_t *>(gout) + 4 * c1;
+            for (uint32_t t = 0; t < ((R1 & 15u) >> 2); ++t)
+                gw[t] = sw[t];
+        }
+        if (NB == 1)
+            __syncthreads(); // the next window reuses the stage
+        else
+            sb = sb ? 0u : SB;
+    }
+    if (tid == 0)
+        pb_count(K, blockIdx.x, nfr, (uint64_t)nfr * flen);
+}
+
+
 } // namespace
 
 extern "C" {
@@ -363,6 +563,46 @@ int pr6v_run(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_fra
         case 17: hipLaunchKernelGGL((pr6v_vline<42, true, 17>), dim3(grid), dim3(PB_WG), lds, st, K); break;
         case 48: hipLaunchKernelGGL((pr6v_vline<42, true, 48>), dim3(grid), dim3(PB_WG), lds, st, K); break;
         case 49: hipLaunchKernelGGL((pr6v_vline<42, true, 49>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    };
+    return pr6_time(ctx, reps, ms, launch);
+}
+
+// the same for pb_fstage_kernel (fixed frames > 128 B): DIAG 0 uncut, 1 no payload bytes, 2 no
+// payload pass (the stage stored as it is), 8 no checksum accumulation
+int pr6v_fst(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, int diag, int reps,
+             double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr6_kargs(ctx, seq, first, n, out, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    if (!K.fst_g || K.fst_g != 16 || !(K.flags & PBK_L4_CSUM))
+        return PBGPU_EINVAL;
+    if (diag & 16)
+    {
+        // pb_orbit_sum reads the orbit table, which the library builds only for packed-frame
+        // sequences: a configs[2]-shaped sequence must have been loaded first
+        if (ctx->d_orbit == nullptr || ctx->d_dlog12 == nullptr)
+            return PBGPU_EINVAL;
+        K.orbit = ctx->d_orbit;
+        K.orbit_tot = ctx->orbit_tot;
+    }
+    const uint32_t grid = (uint32_t)((K.n_frames + K.fst_wgf - 1) / K.fst_wgf);
+    const size_t lds = (size_t)K.fst_nbuf * K.fst_sb + PB_FST_LDS(K.fst_wgf) + 4 * K.fst_wgf + K.lds_pad;
+    hipStream_t st = ctx->stream;
+    auto launch = [&]() -> hipError_t {
+        switch (diag)
+        {
+        case 0: hipLaunchKernelGGL((pr6v_fstage<16, true, 0>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 1: hipLaunchKernelGGL((pr6v_fstage<16, true, 1>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 2: hipLaunchKernelGGL((pr6v_fstage<16, true, 2>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 8: hipLaunchKernelGGL((pr6v_fstage<16, true, 8>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 9: hipLaunchKernelGGL((pr6v_fstage<16, true, 9>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 16: hipLaunchKernelGGL((pr6v_fstage<16, true, 16>), dim3(grid), dim3(PB_WG), lds, st, K); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
