@@ -1,11 +1,17 @@
-// r06_vdiag.hip — where pb_vline_kernel's time goes on the round-6 kernel (tool only, never linked
-// into libpbgpu.so): a copy of the product kernel with compile-time cuts, timed beside the product
-// build and the write-roofline fills on the same buffers, to decide whether cutting its per-chunk
-// VALU work (57 instructions per 16-B chunk, 28 of them the payload bytes) can pay.
-//   DIAG 0: the product kernel (must time as pb_vline_kernel does)
+// r06_vdiag.hip — where pb_vline_kernel's and pb_fstage_kernel's time goes (tool only, never
+// linked into libpbgpu.so): copies of the kernels with compile-time cuts, timed beside the product
+// build and the write-roofline fills on the same buffers.  The pb_vline_kernel copy is the
+// mid-round-6 kernel (57.5 VALU per 16-B chunk); its DIAG 16 / 48 forms prototyped the addressing
+// trim the product now carries (48.5), and its timings are in profiles/r06/vdiag/.
+//   DIAG 0: the copied kernel uncut
 //   DIAG 1: chunks without payload bytes (a state word in every dword; lookups, masks, blend kept)
 //   DIAG 2: no chunk work: constant stores in the kernel's stream geometry (prologue kept)
 //   DIAG 4: no orbit sums in the prologue (the L4 checksum wrong; everything else kept)
+//   DIAG 16: opaque chunk index / bounds; DIAG 32 (with 16: 48): bounds in 1/16 B, image slot by one
+//            v_lshl_add (bit-exact, checked by scripts/r06/vdiag.py)
+// pb_fstage_kernel copy (pr6v_fst): DIAG 1 no payload bytes, 2 no payload pass, 8 no checksum
+// accumulation, 16 L4 sums from the orbit prefix sums in a second wave (needs the orbit table:
+// a packed-frame sequence loaded first; refused otherwise).
 // Built by scripts/r06/build_vdiag.sh into pb-af-xdp_amd/lib/libpbprobe6v.so, driven by
 // scripts/r06/vdiag.py.
 #include "r06_probe.hip"
