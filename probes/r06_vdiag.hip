@@ -576,6 +576,23 @@ int pr6v_run(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_fra
     return pr6_time(ctx, reps, ms, launch);
 }
 
+// the product build (pbk_launch_build) of a packed-frame sequence with its workgroups capped at
+// per_cu per CU by dynamic LDS (0: as the library launches it)
+int pr6v_build_cap(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, uint32_t per_cu,
+                   int reps, double *ms)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    pb_kargs K;
+    int rc = pr6_kargs(ctx, seq, first, n, out, &K);
+    if (rc != PBGPU_OK)
+        return rc;
+    if (!K.vl)
+        return PBGPU_EINVAL;
+    const uint32_t base = (uint32_t)PB_VL_LDS(K.vl_wgf, K.hl == 54 ? 5 : 4, K.vl_nl48, K.vl_nlines);
+    K.lds_pad = per_cu ? lds_cap_pad(base, per_cu) : 0u;
+    return pr6_time(ctx, reps, ms, [&] { return pbk_launch_build(&K, ctx->stream); });
+}
+
 // the same for pb_fstage_kernel (fixed frames > 128 B): DIAG 0 uncut, 1 no payload bytes, 2 no
 // payload pass (the stage stored as it is), 8 no checksum accumulation
 int pr6v_fst(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_frames *out, int diag, int reps,

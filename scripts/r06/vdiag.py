@@ -3,7 +3,8 @@ python3 scripts/r06/vdiag.py [reps] [nbuf] [diag,diag,...]
 configs[2] (2^25 frames) into nbuf buffers alive at once; per buffer, round after round: the product
 build (pr6_build: pb_vline_kernel), its copy with compile-time cuts (DIAG 0 uncut, 1 no payload
 bytes, 2 no chunk work, 4 no orbit sums, 5 = 1 + 4, 6 = 2 + 4) and the write-roofline fills over
-the same bytes (4 KiB per workgroup; 208-KiB regions in 16-KiB steps, the kernel's geometry).
+the same bytes (4 KiB per workgroup; 208-KiB regions in 16-KiB steps, the kernel's geometry); VD_CAPS=4,5,...
+adds the product build with its workgroups capped per CU by dynamic LDS.
 One JSON line per (buffer, variant): medians over the rounds of 10-launch means."""
 import ctypes as C
 import json
@@ -25,6 +26,8 @@ D, U64 = C.c_double, C.c_uint64
 L.pr6v_run.argtypes = [C.c_void_p, C.c_uint16, U64, U64, C.c_void_p, C.c_int, C.c_int, C.POINTER(D)]
 L.pr6_build.argtypes = [C.c_void_p, C.c_uint16, U64, U64, C.c_void_p, C.c_int, C.POINTER(D)]
 L.pr6_fill.argtypes = [C.c_void_p, C.c_void_p, U64, C.c_int, C.c_int, C.POINTER(D)]
+L.pr6v_build_cap.argtypes = [C.c_void_p, C.c_uint16, U64, U64, C.c_void_p, C.c_uint32, C.c_int, C.POINTER(D)]
+CAPS = [int(x) for x in os.environ.get("VD_CAPS", "").split(",") if x]  # product build, workgroups per CU
 
 
 def ok(rc, what):
@@ -67,6 +70,9 @@ for r in range(REPS):
     for b, fb in enumerate(bufs):
         ok(L.pr6_build(ctx.h, 0, 0, n, fb.ptr, 10, C.byref(ms)), "build")
         res.setdefault((b, "product"), []).append(ms.value)
+        for cap in CAPS:
+            ok(L.pr6v_build_cap(ctx.h, 0, 0, n, fb.ptr, cap, 10, C.byref(ms)), f"cap {cap}")
+            res.setdefault((b, f"product cap {cap}/CU"), []).append(ms.value)
         for dg in DIAGS:
             ok(L.pr6v_run(ctx.h, 0, 0, n, fb.ptr, dg, 10, C.byref(ms)), f"diag {dg}")
             res.setdefault((b, f"diag{dg}"), []).append(ms.value)
