@@ -1,4 +1,4 @@
-"""configs[2] kernels side by side in one process on the same buffers (tool only):
+"""configs[2] kernels (or VP_CFG's) side by side in one process on the same buffers (tool only):
 python3 scripts/r06/vp_ab.py [reps] [nbuf] [variants...]
 variants: PBGPU_KERNEL values, or VAR=val[,VAR2=val2] load-time settings, to load (default: "" = the
 library default, and "vpage"); each is
@@ -20,7 +20,7 @@ NBUF = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 VARS = sys.argv[3:] or ["", "vpage"]
 n = 1 << 25
 ctx = GpuContext(0)
-seq = Sequence.from_config(pc.get("c3_udp_var"))
+seq = Sequence.from_config(pc.get(os.environ.get("VP_CFG", "c3_udp_var")))  # VP_CFG: another BASELINE config
 names = {}
 ENV_KEYS = {"PBGPU_KERNEL"}
 for i, v in enumerate(VARS):
