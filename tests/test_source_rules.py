@@ -53,7 +53,9 @@ def test_losing_variants_are_not_compiled_in():
             "PB_VST_XREMAP", "PB_VL_LATE", "PB_VL_SPLIT", "PB_VL_IMGW", "PB_VL_MT", "PB_ORB_LOG12", "PB_ORB_BIDIR",
             "PB_SMALL_DYN", "PB_XS_NT", "PB_SX_NT", "PB_FS_NT", "PB_VL_NT", "xcd_rot", "store_flip", "fst_dbg",
             "PBGPU_XCD_ROT", "PBGPU_STORE_FLIP", "PBGPU_ALLOC_CONTIG", "PBGPU_FST_DBG", "PBGPU_TIMING\"",
-            "PBGPU_XS_TUNE", "PBGPU_LDS_PAD", "tune_xsmall"]
+            "PBGPU_XS_TUNE", "PBGPU_LDS_PAD", "tune_xsmall",
+            # round 6: the page writer's 512-thread and pooled-setup forms (measured, removed)
+            "PBGPU_VP_WGT", "PBGPU_VP_POOL", "vp_wgt", "vp_pool", "pb_vpool_kernel"]
     for name in gone:
         for label, text in (("kernels", k), ("pb_device.h", h), ("pbgpu.cpp", c)):
             assert re.search(r"\b" + re.escape(name) + (r"\b" if name[-1].isalnum() else ""), text) is None, \
