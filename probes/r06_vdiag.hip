@@ -444,7 +444,22 @@ __global__ __launch_bounds__(PB_WG) void pr6v_fstage(pb_kargs K)
             uint32_t x = __umul24(s_z[fr], Mm.x) + Mm.y;
             pb_u32x4 *p = reinterpret_cast<pb_u32x4 *>(stg) + (r >> 4) + mfirst;
             uint32_t o0, o1, o2, o3;
-            for (uint32_t i = 1; i < cnt; ++i)
+            // DIAG 32: the chunk loop unrolled by two (one counter / compare / address step per pair)
+            uint32_t i0 = 1;
+            if (DIAG & 32)
+                for (; i0 + 1u < cnt; i0 += 2u)
+                {
+                    pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+                    acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
+                    p[0] = pb_u32x4{o0, o1, o2, o3};
+                    x = pb_mad24(x, MG.x, mgy);
+                    pb_chunk_payload(K, true, x, 0, 0, 0, 16, o0, o1, o2, o3);
+                    acc = pb_add_halves(pb_add_halves(pb_add_halves(pb_add_halves(acc, o0), o1), o2), o3);
+                    p[G] = pb_u32x4{o0, o1, o2, o3};
+                    p += 2 * G;
+                    x = pb_mad24(x, MG.x, mgy);
+                }
+            for (uint32_t i = i0; i < cnt; ++i)
             {
                 if (DIAG & 1)
                     o0 = o1 = o2 = o3 = x;
@@ -626,6 +641,7 @@ int pr6v_fst(pbgpu_ctx *ctx, uint16_t seq, uint64_t first, uint64_t n, pbgpu_fra
         case 8: hipLaunchKernelGGL((pr6v_fstage<16, true, 8>), dim3(grid), dim3(PB_WG), lds, st, K); break;
         case 9: hipLaunchKernelGGL((pr6v_fstage<16, true, 9>), dim3(grid), dim3(PB_WG), lds, st, K); break;
         case 16: hipLaunchKernelGGL((pr6v_fstage<16, true, 16>), dim3(grid), dim3(PB_WG), lds, st, K); break;
+        case 32: hipLaunchKernelGGL((pr6v_fstage<16, true, 32>), dim3(grid), dim3(PB_WG), lds, st, K); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

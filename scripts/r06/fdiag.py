@@ -2,7 +2,7 @@
 python3 scripts/r06/fdiag.py [reps] [nbuf] [diag,diag,...]
 configs[1]'s 1500-B frames (2^25) into nbuf buffers alive at once; per buffer, round after round:
 the product build, its copy with compile-time cuts (0 uncut, 1 no payload bytes, 2 no payload pass,
-8 no checksum accumulation, 9 = 1 + 8, 16 the L4 sums from the orbit prefix sums in a second wave) and the write-roofline fills over the same bytes.
+8 no checksum accumulation, 9 = 1 + 8, 16 the L4 sums from the orbit prefix sums in a second wave, 32 the chunk loop unrolled by two) and the write-roofline fills over the same bytes.
 One JSON line per (buffer, variant): medians over the rounds of 10-launch means."""
 import ctypes as C
 import json
@@ -43,7 +43,7 @@ ctx.build(0, 777, m, a)
 ctx.sync()
 want = a.packed().copy()
 for dg in DIAGS:
-    if dg not in (0, 16):  # the cuts that keep the bytes
+    if dg not in (0, 16, 32):  # the cuts that keep the bytes
         continue
     ok(L.pr6v_fst(ctx.h, 0, 777, m, b.ptr, dg, 1, C.byref(D())), f"check {dg}")
     ctx.sync()
