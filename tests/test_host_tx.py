@@ -339,10 +339,11 @@ def test_pacing_spreads_the_frames_of_a_batch(libs, kw, gap_s):
     r = _run(libs, _cfg(maxpckts=300, **kw), gpu_batch=100000)
     assert r["err"] == 0 and r["pckts"] == 300
     d = np.diff(r["t"])
-    assert 0.6 * gap_s < np.median(d) < 2.5 * gap_s, np.median(d)
+    assert 0.4 * gap_s < np.median(d) < 4 * gap_s, np.median(d)
     # most frames leave on their own (a launch-granular pacer sends 50-200 back to back, then
-    # waits); a sender delayed by the scheduler catches up with a few at once
-    assert (d > 0.3 * gap_s).mean() > 0.7, (d > 0.3 * gap_s).mean()
+    # waits: under 2% of its gaps are this long); a sender delayed by the scheduler catches up
+    # with a few at once, so the bound leaves room for a loaded machine
+    assert (d > 0.3 * gap_s).mean() > 0.5, (d > 0.3 * gap_s).mean()
 
 
 def test_default_delay_sends_one_frame_per_second_per_thread(libs):
